@@ -1,0 +1,157 @@
+/*
+ * vpt.h -- C ABI of the MI355X volumetric path tracer (libvpt.so).
+ *
+ * Drop-in boundary for the hot path of gabo99cas/minimal_volumetric_path_tracer.  The reference
+ * has no FFI; its hot path is one C++ call per camera sample,
+ *     Color iterativeVPTracerFree(const Ray&, double sigma_a, double sigma_s)   vptShadeMethods.h:1263
+ *     Color MISVPTTracerRecursive(const Ray&, double, double, int depth)        vptShadeMethods.h:1345
+ * made from main()'s OpenMP pixel loop (src/rt.cpp:767-805) with the scene in a global
+ * std::vector<Sphere> (include/Sphere.h:49) and the RNG in a global erand48 state
+ * (include/Vector.h:38).  A GPU cannot be fed one sample per call, so the boundary is lifted to
+ * the pixel loop (vpt_render*), with the per-sample call kept as a batch entry
+ * (vpt_trace_batch).  Implicit globals become explicit arguments; no global state remains.
+ *
+ * Plain C: fixed-width scalars and pointers only.  All functions return VPT_OK (0) or a
+ * negative vpt_status; vpt_last_error() gives a thread-local message for the last failure.
+ */
+#ifndef VPT_H
+#define VPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VPT_ABI_VERSION 1
+
+typedef enum {
+    VPT_OK = 0,
+    VPT_E_INVALID = -1,        /* bad argument (null pointer, size, NaN parameter ...) */
+    VPT_E_TOO_MANY = -2,       /* more spheres than VPT_MAX_SPHERES */
+    VPT_E_NO_EMITTER = -3,     /* reserved */
+    VPT_E_UNSUPPORTED = -4,    /* material id outside {0,1,2,3} */
+    VPT_E_HIP = -5,            /* HIP runtime error (message in vpt_last_error) */
+    VPT_E_IO = -6              /* file could not be written */
+} vpt_status;
+
+#define VPT_MAX_SPHERES 64
+
+/* Byte-identical to the reference's Sphere (include/Sphere.h:12-21; 144 B, offsets r 0, p 8,
+ * c 32, radiance 56, material 80, eta 88, kappa 112, alpha 136), so spheres.data() of a
+ * reference build can be passed as is.  material: 0 Lambert, 1 microfacet conductor, 2 smooth
+ * dielectric (eta 1.5), 3 "volumetric" (only seen by the shadow-ray transmittance).  A sphere
+ * is an emitter when any radiance channel is > 0; r == 0 makes it a point light. */
+typedef struct vpt_sphere {
+    double r;
+    double p[3];
+    double c[3];
+    double radiance[3];
+    int32_t material;
+    int32_t reserved_;
+    double eta[3];
+    double kappa[3];
+    double alpha;
+} vpt_sphere;
+
+/* Reference Ray (include/Ray.h:10-15): origin and direction (callers normalise). */
+typedef struct vpt_ray {
+    double o[3];
+    double d[3];
+} vpt_ray;
+
+typedef enum {
+    VPT_FREE_FLIGHT = 0,       /* iterativeVPTracerFree, vptShadeMethods.h:1263 */
+    VPT_MIS_EQUIANGULAR = 1    /* MISVPTTracerRecursive, vptShadeMethods.h:1345 */
+} vpt_estimator;
+
+typedef enum {
+    VPT_FB_F32 = 0,            /* framebuffer: 3 x float per pixel */
+    VPT_FB_F64 = 1             /* framebuffer: 3 x double per pixel */
+} vpt_fb_format;
+
+/* Homogeneous medium + estimator (src/rt.cpp:794 passes sigma_a = 0.001, sigma_s = 0.009). */
+typedef struct vpt_medium {
+    double sigma_a;
+    double sigma_s;
+    double hg_g;               /* extension: Henyey-Greenstein g; 0 = the reference's isotropic phase */
+    int32_t max_depth;         /* extension: max path vertices; 0 = unbounded (Russian roulette only) */
+    int32_t estimator;         /* vpt_estimator */
+} vpt_medium;
+
+/* One image (or one shard of an image): main() of src/rt.cpp:744-830 made explicit. */
+typedef struct vpt_params {
+    int32_t width, height;     /* src/rt.cpp:752 (1024 x 768) */
+    int32_t spp;               /* src/rt.cpp:784 (argv[1]) */
+    int32_t fb_format;         /* vpt_fb_format */
+    vpt_medium medium;
+    uint64_t seed;             /* image seed; every (pixel, sample) owns an erand48 stream */
+    vpt_ray camera;            /* src/rt.cpp:755: o = (0, 11.2, 214), d = norm(0, -0.042612, -1) */
+    double fov_scale;          /* src/rt.cpp:758-759: 0.5095 */
+    /* Row sharding in FILE order (file row = h-1-y, src/rt.cpp:773).  File rows are cut into
+     * bands of band_rows; this call renders bands band_offset, band_offset + band_stride, ...
+     * and writes them compactly, in increasing file-row order.  Whole image: band_rows = height,
+     * band_stride = 1, band_offset = 0 (vpt_default_params). */
+    int32_t band_rows, band_stride, band_offset;
+    int32_t reserved_;
+} vpt_params;
+
+/* Fills the reference defaults: 1024x768, spp 16, free-flight, sigma 0.001/0.009, camera and
+ * fov of src/rt.cpp:752-759, seed 0x5EED0001, float32 framebuffer, whole image. */
+void vpt_default_params(vpt_params* p);
+
+/* The reference scene (include/Sphere.cpp:11-22): writes min(cap, 10) spheres, returns 10. */
+int vpt_default_scene(vpt_sphere* out, int cap);
+
+/* Number of file rows a params' shard covers (output holds rows * width pixels). */
+int vpt_shard_rows(const vpt_params* p);
+
+/* ---- context: one device, one scene ---- */
+typedef struct vpt_context vpt_context;
+
+int vpt_context_create(int device, vpt_context** out);
+void vpt_context_destroy(vpt_context* ctx);
+/* Copies the scene to the device (replaces the reference's global `spheres`). */
+int vpt_set_scene(vpt_context* ctx, const vpt_sphere* spheres, int n);
+
+/* Renders into a DEVICE buffer on `stream` (a hipStream_t, NULL = default stream); returns
+ * after enqueueing.  d_out: vpt_shard_rows(p) * width * 3 elements of fb_format, the
+ * per-pixel average BEFORE the clamp of src/rt.cpp:803. */
+int vpt_render_device(vpt_context* ctx, const vpt_params* p, void* d_out, void* stream);
+
+/* Same, synchronous, host output buffer. */
+int vpt_render(vpt_context* ctx, const vpt_params* p, void* h_out);
+
+/* The per-sample call itself, batched: rays[i] with erand48 start state states[i] (low 48
+ * bits) through the estimator of `m`; out_rgb[3i..3i+2] = the Color the reference returns,
+ * out_states[i] (optional) = the erand48 state afterwards.  Host pointers; synchronous. */
+int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, const uint64_t* states, int n,
+                    double* out_rgb, uint64_t* out_states);
+
+/* Counting mode: ray-sphere tests (Sphere::intersect calls, include/Sphere.h:27) the render
+ * of `p` performs in the REFERENCE algorithm (shortcuts of this build count what they skip),
+ * plus estimator loop iterations.  Synchronous. */
+int vpt_count_work(vpt_context* ctx, const vpt_params* p, uint64_t* tests, uint64_t* iterations);
+
+/* Start state of one sample's erand48 stream (host-side statement of the device spec). */
+uint64_t vpt_stream_state(uint64_t seed, uint64_t pixel_idx, uint64_t sample);
+
+/* Evaluates the device math library on the GPU: fn 0 sqrt, 1 exp, 2 log, 3 sin, 4 cos, 5 tan,
+ * 6 atan, 7 acos, 8 atan2(x, y), 9 x / y.  Host arrays, synchronous (parity tests). */
+int vpt_math_probe(vpt_context* ctx, int fn, const double* x, const double* y, double* out, int n);
+
+/* PPM writer of main() (src/rt.cpp:812-820): clamp to [0,1] (src/rt.cpp:803), gamma 1/2.2,
+ * int(v*255 + .5) (include/mathUtilities.h:43-45), "P3\n%d %d\n255\n" then "%d %d %d " per
+ * pixel, byte-identical.  rgb: host framebuffer, w*h*3 of fb_format, file order. */
+int vpt_write_ppm(const char* path, const void* rgb, int fb_format, int w, int h);
+/* The same bytes into a caller buffer; returns the byte count (call with buf = NULL to size). */
+int64_t vpt_encode_ppm(const void* rgb, int fb_format, int w, int h, char* buf, int64_t cap);
+
+const char* vpt_last_error(void);
+int vpt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VPT_H */

@@ -1,0 +1,20 @@
+"""MI355X-native volumetric path tracer: the per-pixel radiance loop of
+gabo99cas/minimal_volumetric_path_tracer (src/rt.cpp, include/vptShadeMethods.h) as HIP kernels
+for gfx950 behind a C ABI (include/vpt.h, libvpt.so).  See DESIGN.md."""
+from ._lib import FB_F32, FB_F64, FREE_FLIGHT, MIS_EQUIANGULAR, RAY_DTYPE, SPHERE_DTYPE, VPTError, lib
+from .tracer import (
+    Ray,
+    RenderConfig,
+    Sphere,
+    Tracer,
+    default_scene,
+    encode_ppm,
+    scene,
+    stream_state,
+    write_ppm,
+)
+
+__all__ = [
+    "FB_F32", "FB_F64", "FREE_FLIGHT", "MIS_EQUIANGULAR", "RAY_DTYPE", "SPHERE_DTYPE", "VPTError", "lib",
+    "Ray", "RenderConfig", "Sphere", "Tracer", "default_scene", "encode_ppm", "scene", "stream_state", "write_ppm",
+]

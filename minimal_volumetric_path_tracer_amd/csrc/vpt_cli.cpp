@@ -1,0 +1,87 @@
+/*
+ * vpt_cli.cpp -- the `vpt` program: drop-in for the reference's `./rt <spp>` (src/rt.cpp:744-830).
+ *
+ *   vpt <spp> [--width W] [--height H] [--estimator ff|mis] [--sigma-a A] [--sigma-s S]
+ *             [--g G] [--max-depth D] [--seed N] [--device I] [--fp64] [--out image.ppm]
+ *
+ * With only <spp> it renders the reference's default scene (include/Sphere.cpp:11-22), camera and
+ * medium (src/rt.cpp:752-759,794) at 1024x768 with the free-flight estimator, writes image.ppm
+ * in the reference's exact format and prints "elapsed time: <s>s" like src/rt.cpp:824-827.
+ * Unlike the reference, a missing or bad argument is an error, not undefined behaviour.
+ */
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../../include/vpt.h"
+
+static int usage()
+{
+    std::fprintf(stderr,
+                 "usage: vpt <spp> [--width W] [--height H] [--estimator ff|mis] [--sigma-a A] [--sigma-s S]\n"
+                 "           [--g G] [--max-depth D] [--seed N] [--device I] [--fp64] [--out image.ppm]\n");
+    return 2;
+}
+
+int main(int argc, char** argv)
+{
+    if (argc < 2) return usage();
+    auto start = std::chrono::system_clock::now();
+    vpt_params p;
+    vpt_default_params(&p);
+    char* end = nullptr;
+    long spp = std::strtol(argv[1], &end, 10);
+    if (!end || *end || spp <= 0) return usage();
+    p.spp = (int)spp;
+    std::string out = "image.ppm";
+    int device = 0;
+    for (int i = 2; i < argc; ++i) {
+        std::string a = argv[i];
+        auto need = [&](void) -> const char* {
+            if (i + 1 >= argc) {
+                usage();
+                std::exit(2);
+            }
+            return argv[++i];
+        };
+        if (a == "--width") p.width = std::atoi(need());
+        else if (a == "--height") p.height = std::atoi(need());
+        else if (a == "--estimator") {
+            std::string e = need();
+            if (e == "ff") p.medium.estimator = VPT_FREE_FLIGHT;
+            else if (e == "mis") p.medium.estimator = VPT_MIS_EQUIANGULAR;
+            else return usage();
+        } else if (a == "--sigma-a") p.medium.sigma_a = std::atof(need());
+        else if (a == "--sigma-s") p.medium.sigma_s = std::atof(need());
+        else if (a == "--g") p.medium.hg_g = std::atof(need());
+        else if (a == "--max-depth") p.medium.max_depth = std::atoi(need());
+        else if (a == "--seed") p.seed = std::strtoull(need(), nullptr, 0);
+        else if (a == "--device") device = std::atoi(need());
+        else if (a == "--fp64") p.fb_format = VPT_FB_F64;
+        else if (a == "--out") out = need();
+        else return usage();
+    }
+    p.band_rows = p.height;
+    std::vector<vpt_sphere> scene(VPT_MAX_SPHERES);
+    int n = vpt_default_scene(scene.data(), (int)scene.size());
+    vpt_context* ctx = nullptr;
+    int rc = vpt_context_create(device, &ctx);
+    if (rc == VPT_OK) rc = vpt_set_scene(ctx, scene.data(), n);
+    size_t elem = p.fb_format == VPT_FB_F64 ? sizeof(double) : sizeof(float);
+    std::vector<char> fb((size_t)p.width * p.height * 3 * elem);
+    if (rc == VPT_OK) rc = vpt_render(ctx, &p, fb.data());
+    if (rc == VPT_OK) rc = vpt_write_ppm(out.c_str(), fb.data(), p.fb_format, p.width, p.height);
+    if (rc != VPT_OK) {
+        std::fprintf(stderr, "vpt: error %d: %s\n", rc, vpt_last_error());
+        vpt_context_destroy(ctx);
+        return 1;
+    }
+    vpt_context_destroy(ctx);
+    std::chrono::duration<double> elapsed = std::chrono::system_clock::now() - start;
+    std::cout << "elapsed time: " << elapsed.count() << "s\n";
+    return 0;
+}

@@ -1,0 +1,756 @@
+/*
+ * vpt_device.h -- device side of the volumetric radiance loop (gfx950, FP64).
+ *
+ * Restates, for the GPU, the reference's per-sample estimators
+ *   iterativeVPTracerFree   include/vptShadeMethods.h:1263-1340   (free-flight distance sampling)
+ *   MISVPTTracerRecursive   include/vptShadeMethods.h:1345-1481   (equi-angular + surface MIS)
+ * and everything they reach, with the reference's floating-point
+ * evaluation order (the build compiles with -ffp-contract=off) and the build's portable libm
+ * (vpt_math.h), so that one sample here is bit-identical to the oracle's portable-math build
+ * (oracle/liboracle_vm.so).  Shortcuts taken here are exact (same bits, same random draws):
+ *   - emitter list, MIS light list, material-3 presence: precomputed per scene (host);
+ *   - visibility() from a sphere light (r > 1e-4) toward x: the shadow ray starts at the
+ *     light's centre and hits the light's own surface at t = sqrt(fl(r*r)) = r, so the point is
+ *     visible only when |light - x| < r; otherwise no ray is cast;
+ *   - visibilityVPT() equals visibility() when the scene has no material-3 sphere.
+ * Counting mode (COUNT = true) adds what the reference would have intersected.
+ */
+#ifndef VPT_DEVICE_H
+#define VPT_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vpt_math.h"
+#include "vpt_rng.h"
+#include "vpt_scene.h"
+
+#define VPT_DEV __device__ static inline __attribute__((always_inline))
+#define VPT_PI 3.14159265358979323846
+#define VPT_MAXFLOAT ((double)3.40282346638528859812e+38F) /* MAXFLOAT, vptShadeMethods.h:1287 */
+#define VPT_DBL_MAX 1.7976931348623157e+308                 /* __DBL_MAX__, pathTracingUtilities.h:13 */
+
+namespace vpt {
+
+/* ------------------------------------------------------------------ vectors (Vector.h:10-36) */
+struct dv3 {
+    double x, y, z;
+};
+VPT_DEV dv3 mk(double x, double y, double z) { return dv3{x, y, z}; }
+VPT_DEV dv3 ld3(const double* a) { return dv3{a[0], a[1], a[2]}; }
+VPT_DEV dv3 add(dv3 a, dv3 b) { return dv3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+VPT_DEV dv3 sub(dv3 a, dv3 b) { return dv3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+VPT_DEV dv3 scl(dv3 a, double s) { return dv3{a.x * s, a.y * s, a.z * s}; }
+VPT_DEV dv3 mul(dv3 a, dv3 b) { return dv3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+VPT_DEV double dot(dv3 a, dv3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+VPT_DEV dv3 cross(dv3 a, dv3 b) { return dv3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+VPT_DEV dv3 nrm(dv3 a) { return scl(a, 1.0 / vm_sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); }
+
+struct Counters {
+    uint64_t tests;
+    uint64_t iterations;
+};
+
+/* Per-sample random stream + work counters.  HG g rides along (phase extension). */
+template <bool COUNT>
+struct Sampler {
+    uint64_t X;
+    double g;
+    Counters cnt;
+    __device__ __forceinline__ double next() { return vpt_erand48(&X); }
+    __device__ __forceinline__ void tests(int n)
+    {
+        if (COUNT) cnt.tests += (uint64_t)n;
+    }
+};
+
+/* ------------------------------------------------------------------ geometry */
+/* Sphere::intersect (include/Sphere.h:27-37) folded into intersect()
+ * (include/pathTracingUtilities.h:12-36).  The sphere index is wave-uniform, so the scene
+ * record comes through scalar loads. */
+template <bool COUNT>
+VPT_DEV int scene_intersect(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, double& t,
+                            int& id, bool skip3)
+{
+    double tmin = VPT_DBL_MAX;
+    int contact = 0;
+    const int n = S->n;
+    for (int i = 0; i < n; ++i) {
+        const GeoSphere g = S->geo[i];
+        if (skip3 && g.mat3) continue;
+        double ocx = o.x - g.px, ocy = o.y - g.py, ocz = o.z - g.pz;
+        double b = ocx * d.x + ocy * d.y + ocz * d.z;
+        double cc = ocx * ocx + ocy * ocy + ocz * ocz;
+        double det = b * b - cc + g.r2;
+        double tact = 0.0;
+        if (det >= 0) {
+            double sq = vm_sqrt(det);
+            double t2 = -b + sq;
+            double t1 = -b - sq;
+            tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
+        }
+        if (tact > 0 && vm_fabs(tact) > 0.0001) {
+            contact = 1;
+            if (tact < tmin) {
+                tmin = tact;
+                id = i;
+            }
+        }
+    }
+    smp.tests(skip3 ? S->n_non3 : n);
+    if (contact) {
+        t = tmin;
+        return 1;
+    }
+    t = 0;
+    return 0;
+}
+
+/* visibility (include/pathTracingUtilities.h:39-53), skip3 = visibilityVPT
+ * (include/volumetricBasicFunctions.h:92-106).  light_r: radius of the light sphere when the
+ * light point is a sphere centre (exact shortcut, header comment), negative otherwise. */
+template <bool COUNT>
+VPT_DEV int visibility(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 light, dv3 x, bool skip3,
+                       double light_r, bool light_is3)
+{
+    dv3 lx = sub(light, x);
+    double distance = vm_sqrt(dot(lx, lx));
+    if (light_r > 0.0001 && !(skip3 && light_is3) && !(distance < light_r)) {
+        smp.tests(skip3 ? S->n_non3 : S->n);
+        return 0;
+    }
+    lx = nrm(lx);
+    lx = scl(lx, -1);
+    int id = 0;
+    double t;
+    scene_intersect(S, smp, light, lx, t, id, skip3);
+    return (t > distance || t == 0);
+}
+
+/* coordinateSystem, include/mathUtilities.h:10-19 */
+VPT_DEV void coord_system(dv3 n, dv3& s, dv3& t)
+{
+    if (vm_fabs(n.x) > vm_fabs(n.y)) {
+        double invLen = 1.0 / vm_sqrt(n.x * n.x + n.z * n.z);
+        t = mk(n.z * invLen, 0.0, -n.x * invLen);
+    } else {
+        double invLen = 1.0 / vm_sqrt(n.y * n.y + n.z * n.z);
+        t = mk(0.0, n.z * invLen, -n.y * invLen);
+    }
+    s = cross(t, n);
+}
+
+/* coordinateTraspose, include/mathUtilities.h:21-30 */
+VPT_DEV dv3 to_local(dv3 n, dv3 w)
+{
+    dv3 s, t;
+    coord_system(n, s, t);
+    return mk(dot(s, w), dot(t, w), dot(n, w));
+}
+
+VPT_DEV dv3 from_local(dv3 n, double x1, double y1, double z1)
+{
+    dv3 s, t;
+    coord_system(n, s, t);
+    return add(add(scl(s, x1), scl(t, y1)), scl(n, z1));
+}
+
+/* transmitance, include/volumetricBasicFunctions.h:14-21 */
+VPT_DEV double transmitance(dv3 a, dv3 b, double sigma_t)
+{
+    dv3 aux = sub(b, a);
+    double d = vm_sqrt(dot(aux, aux));
+    return vm_exp(sigma_t * d * -1.0);
+}
+
+/* multipleT, include/volumetricBasicFunctions.h:26-57 (material-3 spheres only) */
+template <bool COUNT>
+VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 x1, dv3 x2, double sigma_t)
+{
+    double T = 1;
+    dv3 w = nrm(sub(x2, x1));
+    for (int i = 0; i < S->n; ++i) {
+        const GeoSphere g = S->geo[i];
+        if (!g.mat3) continue;
+        smp.tests(1);
+        double ocx = x1.x - g.px, ocy = x1.y - g.py, ocz = x1.z - g.pz;
+        double b = ocx * w.x + ocy * w.y + ocz * w.z;
+        double det = b * b - (ocx * ocx + ocy * ocy + ocz * ocz) + g.r2;
+        double ta = 0.0, tb = 0.0;
+        if (!(det < 0)) {
+            double sq = vm_sqrt(det);
+            tb = -b + sq;
+            ta = -b - sq;
+        }
+        if (tb < 0) T = T * vm_exp(-sigma_t * ta);
+        if (tb - ta > 0) T = T * vm_exp(-sigma_t * (tb - ta));
+    }
+    return T;
+}
+
+/* ------------------------------------------------------------------ sampling */
+VPT_DEV dv3 dir_from_angles(dv3 n, double theta, double phi)
+{
+    double st, ct, sp, cp;
+    vm_sincos(theta, &st, &ct);
+    vm_sincos(phi, &sp, &cp);
+    return nrm(from_local(n, st * cp, st * sp, ct));
+}
+
+/* solidAngle(wc, costheta_max), include/samplingFunctions.h:65-82 */
+template <bool COUNT>
+VPT_DEV dv3 solid_angle_dir(Sampler<COUNT>& smp, dv3 wc, double cmax)
+{
+    double e0 = smp.next();
+    double theta = vm_acos((1 - e0) + e0 * cmax);
+    double phi = 2 * VPT_PI * smp.next();
+    return dir_from_angles(wc, theta, phi);
+}
+
+/* solidAngleProb, include/samplingFunctions.h:85-87 */
+VPT_DEV double solid_angle_prob(double cmax) { return 1 / (2 * VPT_PI * (1 - cmax)); }
+/* hemiCosineProb, include/samplingFunctions.h:92-94 */
+VPT_DEV double hemi_cosine_prob(double c) { return c * 1 / VPT_PI; }
+
+/* cosineHemispheric, include/samplingFunctions.h:47-62 */
+template <bool COUNT>
+VPT_DEV dv3 cosine_hemispheric(Sampler<COUNT>& smp, dv3 n)
+{
+    double theta = vm_acos(vm_sqrt(1 - smp.next()));
+    double phi = 2 * VPT_PI * smp.next();
+    return dir_from_angles(n, theta, phi);
+}
+
+/* isotropicPhaseSample, include/vptSamplingFunctions.h:34-47 (g == 0); Henyey-Greenstein
+ * extension around the propagation direction din otherwise. */
+template <bool COUNT>
+VPT_DEV dv3 phase_sample(Sampler<COUNT>& smp, dv3 din)
+{
+    double xi1 = smp.next();
+    double xi2 = smp.next();
+    double g = smp.g;
+    if (g == 0.0) {
+        double theta = vm_acos(1 - 2 * xi1);
+        double phi = 2 * VPT_PI * xi2;
+        double st, ct, sp, cp;
+        vm_sincos(theta, &st, &ct);
+        vm_sincos(phi, &sp, &cp);
+        return nrm(mk(st * cp, st * sp, ct));
+    }
+    double sq = (1.0 - g * g) / (1.0 - g + 2.0 * g * xi1);
+    double ct = (1.0 + g * g - sq * sq) / (2.0 * g);
+    double st2 = 1.0 - ct * ct;
+    double st = st2 > 0.0 ? vm_sqrt(st2) : 0.0;
+    double phi = 2 * VPT_PI * xi2;
+    double sp, cp;
+    vm_sincos(phi, &sp, &cp);
+    return nrm(from_local(din, st * cp, st * sp, ct));
+}
+
+/* isotropicPhaseFunction (include/volumetricBasicFunctions.h:59-62) or HG value */
+VPT_DEV double phase_value(double g, dv3 din, dv3 wl)
+{
+    if (g == 0.0) return 1 / (4 * VPT_PI);
+    double mu = dot(din, wl);
+    double den = 1.0 + g * g - 2.0 * g * mu;
+    return (1.0 - g * g) / (4 * VPT_PI * (den * vm_sqrt(den)));
+}
+
+/* ------------------------------------------------------------------ microfacet (microFacetUtilities.h) */
+/* fresnelSpectre, :11-18 */
+VPT_DEV double fresnel_spectre(double cosine, double sine, double eta, double kappa)
+{
+    double a2b2 = vm_sqrt((eta * eta - kappa * kappa - sine * sine) * (eta * eta - kappa * kappa - sine * sine) +
+                          4 * eta * eta * kappa * kappa);
+    double a = vm_sqrt(0.5 * (a2b2 + eta * eta - kappa * kappa - sine * sine));
+    double perpendicular = (a2b2 + cosine * cosine - 2 * a * cosine) / (a2b2 + cosine * cosine + 2 * a * cosine);
+    double parallel = perpendicular *
+                      (a2b2 * cosine * cosine + sine * sine * sine * sine - 2 * a * cosine * sine * sine) /
+                      (a2b2 * cosine * cosine + sine * sine * sine * sine + 2 * a * cosine * sine * sine);
+    return 0.5 * (parallel + perpendicular);
+}
+
+/* fresnel, :21-29 */
+VPT_DEV dv3 fresnel(double cw, dv3 eta, dv3 kappa)
+{
+    double sw = vm_sqrt(1 - cw * cw);
+    return mk(fresnel_spectre(cw, sw, eta.x, kappa.x), fresnel_spectre(cw, sw, eta.y, kappa.y),
+              fresnel_spectre(cw, sw, eta.z, kappa.z));
+}
+
+/* NDF (Beckmann), :34-45 */
+VPT_DEV double ndf(double cosine, double alpha)
+{
+    if (cosine >= 0) {
+        double sine = vm_sqrt(1 - cosine * cosine);
+        double fac1 = VPT_PI * alpha * alpha * cosine * cosine * cosine * cosine;
+        double tang = sine / cosine;
+        double fac2 = vm_exp((-1 * tang * tang) / (alpha * alpha));
+        return (1 / fac1) * fac2;
+    }
+    return 0;
+}
+
+/* Gn, :47-61 */
+VPT_DEV double g1(dv3 n, dv3 wv, dv3 wh, double alpha)
+{
+    double sn = vm_sqrt(1 - dot(n, wv) * dot(n, wv));
+    double tn = sn / (dot(n, wv));
+    double a = 1 / (alpha * tn);
+    if (((dot(wv, wh)) / (dot(wv, n))) > 0) {
+        if (a < 1.6) {
+            double num = 3.535 * a + 2.181 * a * a;
+            double den = 1 + 2.276 * a + 2.577 * a * a;
+            return num / den;
+        }
+        return 1;
+    }
+    return 0;
+}
+
+/* vectorFacet, :71-84 */
+template <bool COUNT>
+VPT_DEV dv3 vector_facet(Sampler<COUNT>& smp, double alpha)
+{
+    double theta = vm_atan(vm_sqrt(-alpha * alpha * vm_log(1 - smp.next())));
+    double phi = 2 * VPT_PI * smp.next();
+    double st, ct, sp, cp;
+    vm_sincos(theta, &st, &ct);
+    vm_sincos(phi, &sp, &cp);
+    return nrm(mk(st * cp, st * sp, ct));
+}
+
+/* microFacetProb, :86-92 */
+VPT_DEV double microfacet_prob(dv3 wo, dv3 wh, double alpha, dv3 n)
+{
+    double num = dot(wh, n);
+    double den = 4 * vm_fabs(dot(wo, wh));
+    return ndf(dot(wh, n), alpha) * num / den;
+}
+
+/* frMicroFacet, :95-100 (G_smith :63-68) */
+VPT_DEV dv3 fr_microfacet(dv3 eta, dv3 kappa, dv3 wi, dv3 wh, dv3 wo, double alpha, dv3 n)
+{
+    double den = (4 * vm_fabs(dot(n, wi)) * vm_fabs(dot(n, wo)));
+    double G = g1(n, wi, wh, alpha) * g1(n, wo, wh, alpha);
+    return scl(scl(scl(fresnel(dot(wi, wh), eta, kappa), ndf(dot(n, wh), alpha)), G), (1 / den));
+}
+
+/* fresnelDie, :107-112 */
+VPT_DEV double fresnel_die(double etai, double etat, double ct, double ci)
+{
+    double parallel = ((etat * ci - etai * ct) / (etat * ci + etai * ct)) * ((etat * ci - etai * ct) / (etat * ci + etai * ct));
+    double perpendicular =
+        ((etai * ci - etat * ct) / (etai * ci + etat * ct)) * ((etai * ci - etat * ct) / (etai * ci + etat * ct));
+    return 0.5 * (parallel + perpendicular);
+}
+
+/* reflexDielectric, :117-120 */
+VPT_DEV dv3 reflex_dielectric(dv3 wi, dv3 n) { return add(scl(wi, -1), scl(scl(n, dot(n, wi)), 2)); }
+
+/* refraxDielectric, :123-141 */
+VPT_DEV dv3 refrax_dielectric(double etai, double etat, dv3 wi, dv3 n)
+{
+    dv3 wil = to_local(n, wi);
+    double ratio = etat / etai * -1;
+    double cosinei = dot(wi, n);
+    double invratio = etai / etat;
+    double cosinet = vm_sqrt(1 - invratio * invratio * (1 - cosinei * cosinei)) - 1;
+    return from_local(n, wil.x * ratio, wil.y * ratio, cosinet);
+}
+
+/* ------------------------------------------------------------------ shading records */
+VPT_DEV dv3 sph_c(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].c); }
+VPT_DEV dv3 sph_rad(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].radiance); }
+VPT_DEV dv3 sph_p(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].p); }
+
+/* rayTracer, include/pathTracingUtilities.h:56-64 */
+template <bool COUNT>
+VPT_DEV dv3 ray_tracer(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 x, dv3 wi, int& sourceid)
+{
+    double t;
+    int id = 0;
+    if (!scene_intersect(S, smp, x, wi, t, id, false)) return mk(0, 0, 0);
+    sourceid = id;
+    return sph_rad(S, id);
+}
+
+/* cosinethetaMax, include/pathTracingUtilities.h:66-73 */
+VPT_DEV double cos_theta_max(const DevScene* __restrict__ S, int sid, dv3 x)
+{
+    double radio = S->sph[sid].r;
+    dv3 cx = sub(sph_p(S, sid), x);
+    double normcx = vm_sqrt(dot(cx, cx));
+    return vm_sqrt(1 - (radio / normcx) * (radio / normcx));
+}
+
+/* ------------------------------------------------------------------ light transport */
+/* microfacet (BSDF-sampled light), include/samplingFunctions.h:97-118 */
+template <bool COUNT>
+VPT_DEV dv3 microfacet_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 x, dv3 wo, dv3 wh, dv3 n,
+                             int obj, double alpha, int& idsource)
+{
+    const dv3 nl = mk(0, 0, 1);
+    int sourceid = 0;
+    wo = scl(wo, -1);
+    wo = nrm(to_local(n, wo));
+    dv3 wi = nrm(add(scl(wo, -1), scl(scl(wh, 2), dot(wh, wo))));
+    dv3 wig = nrm(from_local(n, wi.x, wi.y, wi.z));
+    dv3 Le = ray_tracer(S, smp, x, wig, sourceid);
+    idsource = sourceid;
+    dv3 fr = fr_microfacet(ld3(S->sph[obj].eta), ld3(S->sph[obj].kappa), wi, wh, wo, alpha, nl);
+    return scl(scl(mul(Le, fr), dot(mk(0, 0, 1), wi)), (1 / microfacet_prob(wo, wh, alpha, nl)));
+}
+
+/* muestreoSA (include/samplingFunctions.h:238-247) + solidAngle 9-arg (:163-206) */
+template <bool COUNT>
+VPT_DEV dv3 light_sample_sa(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int light, dv3 x, int obj, int omat,
+                            dv3 n, dv3 wray, dv3& aux, double& cmax_out, double alpha)
+{
+    dv3 cx = sub(sph_p(S, light), x);
+    double normcx = vm_sqrt(dot(cx, cx));
+    cx = scl(cx, (1 / normcx));
+    double lr = S->sph[light].r;
+    double cmax = vm_sqrt(1 - (lr / normcx) * (lr / normcx));
+    cmax_out = cmax;
+    dv3 wolocal = scl(wray, -1);
+    dv3 wi = solid_angle_dir(smp, cx, cmax);
+    aux = wi;
+    dv3 wilocal = nrm(to_local(n, wi));
+    wolocal = nrm(to_local(n, wolocal));
+    dv3 wh = nrm(add(wilocal, wolocal));
+    dv3 fr;
+    if (omat == 0) fr = scl(sph_c(S, obj), (1 / VPT_PI));
+    else if (omat == 2) fr = mk(0, 0, 0);
+    else fr = fr_microfacet(ld3(S->sph[obj].eta), ld3(S->sph[obj].kappa), wilocal, wh, wolocal, alpha, mk(0, 0, 1));
+    double t;
+    int id = 0;
+    scene_intersect(S, smp, x, wi, t, id, false);
+    dv3 Le = (light == id) ? sph_rad(S, id) : mk(0, 0, 0);
+    return scl(scl(mul(Le, fr), dot(n, wi)), (1 / solid_angle_prob(cmax)));
+}
+
+/* softDielectric, include/samplingFunctions.h:209-235 */
+template <bool COUNT>
+VPT_DEV dv3 soft_dielectric(const DevScene* __restrict__ S, Sampler<COUNT>& smp, double etat, double etai, dv3 wi,
+                            dv3 n, dv3 x, int& idsource)
+{
+    dv3 Ld;
+    int sourceid = 0;
+    dv3 wt = nrm(refrax_dielectric(etai, etat, wi, n));
+    double F = fresnel_die(etai, etat, dot(n, wt), dot(n, wi));
+    if (smp.next() < F) {
+        dv3 wr = nrm(reflex_dielectric(wi, n));
+        Ld = scl(ray_tracer(S, smp, x, wr, sourceid), (1 / vm_fabs(dot(n, wr))));
+    } else {
+        double ratio = etat / etai;
+        Ld = scl(scl(scl(ray_tracer(S, smp, x, wt, sourceid), (1 / vm_fabs(dot(n, wt)))), ratio), ratio);
+    }
+    idsource = sourceid;
+    return Ld;
+}
+
+/* powerHeuristics, include/misSamplingFunctions.h:12-16 */
+VPT_DEV double power_heuristic(double f, double g)
+{
+    double f2 = f * f;
+    double g2 = g * g;
+    return f2 / (f2 + g2);
+}
+
+/* MISv2, include/misSamplingFunctions.h:96-170 */
+template <bool COUNT>
+VPT_DEV dv3 mis_v2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray, double alpha,
+                   double sigma_t)
+{
+    const int omat = S->sph[obj].material;
+    dv3 mc = mk(0, 0, 0), g;
+    dv3 wiLight = mk(0, 0, 0), wiBDRF = mk(0, 0, 0);
+    double wg, fpdf = 0, gpdf = 0, cmax = 0;
+    int sourceid = 0, sourceid2 = 0;
+    dv3 wo = scl(wray, -1);
+    for (int k = 0; k < S->n_mis; ++k) {  /* spheres with r > 0 && radiance.x > 0, in index order */
+        const int light = S->mis_light[k];
+        dv3 f = light_sample_sa(S, smp, light, x, obj, omat, n, wray, wiLight, cmax, alpha);
+        f = scl(f, transmitance(x, sph_p(S, light), sigma_t));
+        fpdf = solid_angle_prob(cmax);
+        if (omat == 0) {
+            gpdf = hemi_cosine_prob(dot(n, wiLight));
+        } else if (omat == 2) {
+            dv3 wt = nrm(refrax_dielectric(1.0, 1.5, wo, n));
+            gpdf = fresnel_die(1.0, 1.5, dot(n, wt), dot(n, wo));
+            if (smp.next() > gpdf) gpdf = 1 - gpdf;
+        } else {
+            dv3 wh = nrm(add(wiLight, wo));
+            gpdf = microfacet_prob(wo, wh, alpha, n);
+        }
+        double wf = power_heuristic(fpdf, gpdf);
+        mc = add(mc, scl(f, wf));
+    }
+    if (omat == 0) {
+        /* uniform(), include/samplingFunctions.h:250-261 */
+        dv3 wi = nrm(cosine_hemispheric(smp, n));
+        dv3 Le = ray_tracer(S, smp, x, wi, sourceid);
+        g = add(mk(0, 0, 0), scl(scl(mul(Le, scl(sph_c(S, obj), (1 / VPT_PI))), dot(n, wi)), (1 / hemi_cosine_prob(dot(n, wi)))));
+        wiBDRF = wi;
+        gpdf = hemi_cosine_prob(dot(n, wiBDRF));
+        if (g.x > 0 && g.y > 0 && g.z > 0) {
+            cmax = cos_theta_max(S, sourceid, x);
+            fpdf = solid_angle_prob(cmax);
+            wg = power_heuristic(gpdf, fpdf);
+        } else {
+            wg = 0;
+        }
+    } else if (omat == 2) {
+        g = soft_dielectric(S, smp, 1.5, 1.0, wo, n, x, sourceid);
+        if (g.x > 0 && g.y > 0 && g.z > 0) {
+            cmax = cos_theta_max(S, sourceid, x);
+            fpdf = solid_angle_prob(cmax);
+            wg = power_heuristic(gpdf, fpdf); /* gpdf: stale value from the light loop (reference) */
+        } else {
+            wg = 0;
+        }
+    } else {
+        dv3 wh = vector_facet(smp, alpha);
+        wo = nrm(to_local(n, wo));
+        g = microfacet_light(S, smp, x, wray, wh, n, obj, alpha, sourceid2);
+        gpdf = microfacet_prob(wo, wh, alpha, mk(0, 0, 1));
+        if (g.x > 0) cmax = cos_theta_max(S, sourceid2, x);
+        fpdf = solid_angle_prob(cmax);
+        wg = power_heuristic(gpdf, fpdf);
+    }
+    return add(mc, scl(g, wg));
+}
+
+/* bdsf (continuation sample), include/vptShadeMethods.h:16-59 */
+template <bool COUNT>
+VPT_DEV dv3 bdsf(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3& aux, dv3 wray, dv3 n, double& prob, int id)
+{
+    const int mat = S->sph[id].material;
+    dv3 wi, fs1 = mk(0, 0, 0);
+    dv3 wo = scl(wray, -1);
+    if (mat == 0) {
+        wi = cosine_hemispheric(smp, n);
+        fs1 = scl(sph_c(S, id), (1 / VPT_PI));
+        prob = hemi_cosine_prob(dot(n, wi));
+        aux = wi;
+    } else if (mat == 2) {
+        dv3 wt = nrm(refrax_dielectric(1.0, 1.5, wo, n));
+        double F = fresnel_die(1.0, 1.5, dot(n, wt), dot(n, wo));
+        if (smp.next() < F) {
+            wi = nrm(reflex_dielectric(wo, n));
+            fs1 = scl(scl(mk(1, 1, 1), (1 / dot(n, wi))), F);
+            prob = F;
+        } else {
+            wi = wt;
+            fs1 = scl(scl(scl(scl(mk(1, 1, 1), (1 / dot(n, wi))), (1 - F)), 1.5), 1.5);
+            prob = 1 - F;
+        }
+        aux = wi;
+    } else if (mat == 1) {
+        double alpha = S->sph[id].alpha;
+        dv3 whl = vector_facet(smp, alpha);
+        dv3 wh = from_local(n, whl.x, whl.y, whl.z);
+        wi = add(scl(wo, -1), scl(scl(wh, 2), dot(wh, wo)));
+        fs1 = fr_microfacet(ld3(S->sph[id].eta), ld3(S->sph[id].kappa), wi, wh, wo, alpha, n);
+        prob = microfacet_prob(wo, wh, alpha, n);
+        aux = wi;
+    }
+    return fs1;
+}
+
+/* pLight (point-light NEE at a surface), include/vptShadeMethods.h:62-91 */
+template <bool COUNT>
+VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray, int src,
+                    double alpha)
+{
+    const dv3 I = sph_rad(S, src);
+    const dv3 light = sph_p(S, src);
+    const double lr = S->sph[src].r;
+    const bool l3 = S->geo[src].mat3;
+    dv3 Le;
+    if (visibility(S, smp, light, x, false, lr, l3)) {
+        Le = scl(I, (1 / (dot(sub(light, x), sub(light, x)))));
+    } else if (S->n_mat3 == 0) {
+        smp.tests(S->n);  /* visibilityVPT == visibility (no material-3 sphere): same miss */
+        Le = mk(0, 0, 0);
+    } else if (visibility(S, smp, light, x, true, lr, l3)) {
+        Le = scl(I, (1 / (dot(sub(light, x), sub(light, x)))));
+        Le = scl(Le, multiple_t(S, smp, x, light, 0.05 + 0.009));
+    } else {
+        Le = mk(0, 0, 0);
+    }
+    dv3 wi = nrm(sub(light, x));
+    dv3 wo = scl(wray, -1);
+    wo = to_local(n, wo);
+    wi = to_local(n, wi);
+    wi = nrm(wi);
+    wo = nrm(wo);
+    dv3 wh = nrm(add(wi, wo));
+    dv3 fr;
+    if (S->sph[obj].material == 1)
+        fr = fr_microfacet(ld3(S->sph[obj].eta), ld3(S->sph[obj].kappa), wi, wh, wo, alpha, mk(0, 0, 1));
+    else
+        fr = scl(sph_c(S, obj), (1 / VPT_PI));
+    return scl(mul(Le, fr), dot(n, nrm(sub(light, x))));
+}
+
+/* freeSingleScattering (with_sigma = false), include/volumetricBasicFunctions.h:284-340, and
+ * singleScattering (with_sigma = true), :225-281.  din: propagation direction (HG only). */
+template <bool COUNT>
+VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
+                              double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource)
+{
+    const double lr = S->sph[src].r;
+    const dv3 lp = sph_p(S, src);
+    const dv3 rad = sph_rad(S, src);
+    dv3 Ld = mk(0, 0, 0);
+    if (lr == 0) {
+        if (visibility(S, smp, lp, xt, false, -1.0, false)) {
+            double distanceLight = dot(sub(lp, xt), sub(lp, xt));
+            dv3 Le = scl(rad, (1 / distanceLight));
+            double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, nrm(sub(lp, xt)));
+            dv3 Ls = scl(scl(Le, transmitance(xt, lp, sigma_t)), ph);
+            if (with_sigma) Ld = scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
+            else Ld = scl(Ls, (1 / probSource));
+        }
+    }
+    dv3 wc = sub(lp, xt);
+    double mag = vm_sqrt(dot(wc, wc));
+    wc = scl(wc, (1 / mag));
+    double cmax = vm_sqrt(1 - lr / mag * (lr / mag));
+    dv3 wl = solid_angle_dir(smp, wc, cmax);
+    double prob_wl = solid_angle_prob(cmax);
+    double tdist;
+    int idHit = 0;
+    scene_intersect(S, smp, xt, wl, tdist, idHit, false);
+    if (src == idHit) {
+        double it = vm_exp(sigma_t * tdist * -1.0);
+        double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, wl);
+        dv3 Ls = scl(scl(rad, it), ph);
+        if (with_sigma) Ld = scl(scl(scl(scl(Ls, trxt), sigma_s), (1 / prob_wl)), (1 / probSource));
+        else Ld = scl(scl(Ls, (1 / prob_wl)), (1 / probSource));
+    }
+    return Ld;
+}
+
+/* equiAngularParams2 (include/volumetricBasicFunctions.h:209-223) */
+template <bool COUNT>
+VPT_DEV double equiangular_params2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int src, double tMax, dv3 ro,
+                                   dv3 rd, double& D, double& ta, double& tb, double& sample_t)
+{
+    dv3 dv = sub(sph_p(S, src), ro);
+    double dvn = vm_sqrt(dot(dv, dv));
+    double proj = dot(dv, rd) / dot(rd, rd);
+    D = vm_sqrt(dvn * dvn - proj * proj);
+    ta = vm_atan2(0.0 - proj, D);
+    tb = vm_atan2(tMax - proj, D);
+    double x = smp.next();
+    sample_t = D * vm_tan((1 - x) * ta + x * tb);
+    return sample_t + proj;
+}
+
+/* equiAngularProb, include/vptSamplingFunctions.h:60-62 */
+VPT_DEV double equiangular_prob(double D, double ta, double tb, double s) { return D / vm_fabs(tb - ta) / (s * s + D * D); }
+
+/* ------------------------------------------------------------------ estimators */
+struct Medium {
+    double sigma_a, sigma_s, g;
+    int max_depth;
+};
+
+/* iterativeVPTracerFree (EST = 0), include/vptShadeMethods.h:1263-1340, and
+ * MISVPTTracerRecursive (EST = 1), :1345-1481, as one forward loop with a running throughput
+ * (the reference's FF stack holds at most one frame; the MIS recursion is linear). */
+template <int EST, bool COUNT>
+__device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, const Medium& m)
+{
+    dv3 beta = mk(1, 1, 1);
+    dv3 L = mk(0, 0, 0);
+    const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
+    const double sigma_t = sigma_a + sigma_s;
+    const double continueprob = 0.6;
+    const double q = 1 - continueprob;
+    const int count = S->n_emit;
+    for (int depth = 0;; ++depth) {
+        if (m.max_depth > 0 && depth >= m.max_depth) break;
+        if (COUNT) smp.cnt.iterations++;
+        if (smp.next() < q) break;
+        double t;
+        int id = 0;
+        if (!scene_intersect(S, smp, o, d, t, id, false)) t = VPT_MAXFLOAT;
+        dv3 xs = add(o, scl(d, t));
+        dv3 nx = nrm(sub(xs, sph_p(S, id)));
+        if (count == 0) break;
+        double probSource = 1.0 / count;
+        int idsource = S->emit[(int)(smp.next() * count)];
+        if (EST == 0) {
+            double dist = -vm_log(1 - smp.next()) / sigma_t;  /* freeFlightSample, vptSamplingFunctions.h:11-14 */
+            if (dist > t) {
+                if (S->geo[id].emitter) {
+                    if (depth == 0) L = mul(sph_rad(S, id), beta);
+                    break;
+                }
+                double alpha = S->sph[id].alpha;
+                double Trs = transmitance(xs, sph_p(S, idsource), sigma_t);
+                dv3 Ldp = scl(scl(p_light(S, smp, id, xs, nx, d, idsource, alpha), Trs), (1 / probSource));
+                dv3 Ld = mis_v2(S, smp, id, xs, nx, d, alpha, sigma_t);
+                dv3 wi = mk(0, 0, 0);
+                double pdf = 0;
+                dv3 fs = bdsf(S, smp, wi, d, nx, pdf, id);
+                wi = nrm(wi);
+                double cosine = dot(nx, wi);
+                L = add(L, scl(mul(add(Ldp, Ld), beta), (1 / continueprob)));
+                beta = scl(scl(scl(mul(beta, fs), (1 / continueprob)), cosine), (1 / pdf));
+                o = xs;
+                d = wi;
+            } else {
+                dv3 xt = add(o, scl(d, dist));
+                dv3 Ld = single_scattering(S, smp, xt, d, idsource, sigma_t, false, sigma_s, 1.0, probSource);
+                dv3 wi = phase_sample(smp, d);
+                L = add(L, scl(scl(mul(Ld, beta), (sigma_s / sigma_t)), (1 / continueprob)));
+                beta = scl(scl(beta, (sigma_s / sigma_t)), (1 / continueprob));
+                o = xt;
+                d = wi;
+            }
+        } else {
+            double D = 0, ta = 0, tb = 0, sd = 0;
+            double psurf = vm_exp(sigma_t * t * -1.0);
+            double d_final = equiangular_params2(S, smp, idsource, t, o, d, D, ta, tb, sd);
+            double pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
+            if (smp.next() < psurf) {
+                if (S->geo[id].emitter) {
+                    if (depth == 0) L = sph_rad(S, id);
+                    break;
+                }
+                double alpha = S->sph[id].alpha;
+                double Trs = transmitance(xs, sph_p(S, idsource), sigma_t);
+                dv3 Ldp = scl(scl(p_light(S, smp, id, xs, nx, d, idsource, alpha), Trs), (1 / probSource));
+                dv3 Ld = mis_v2(S, smp, id, xs, nx, d, alpha, sigma_t);
+                dv3 wi = mk(0, 0, 0);
+                double spdf = 0;
+                dv3 fs = bdsf(S, smp, wi, d, nx, spdf, id);
+                wi = nrm(wi);
+                double cosine = dot(nx, wi);
+                L = add(L, mul(beta, scl(add(Ldp, Ld), (1 / continueprob))));
+                beta = scl(scl(scl(mul(beta, fs), (1 / continueprob)), cosine), (1 / spdf));
+                o = xs;
+                d = wi;
+            } else {
+                dv3 xt = add(o, scl(d, d_final));
+                double T = transmitance(o, xt, sigma_t);
+                dv3 Ld = single_scattering(S, smp, xt, d, idsource, sigma_t, true, sigma_s, T, probSource);
+                dv3 wi = phase_sample(smp, d);
+                L = add(L, mul(beta, scl(scl(Ld, (1 / pdf)), (1 / continueprob))));
+                beta = scl(scl(scl(scl(beta, sigma_s), T), (1 / continueprob)), (1 / pdf));
+                o = xt;
+                d = wi;
+            }
+        }
+    }
+    return L;
+}
+
+}  // namespace vpt
+
+#endif

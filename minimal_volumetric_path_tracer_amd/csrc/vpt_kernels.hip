@@ -1,0 +1,417 @@
+/*
+ * vpt_kernels.hip -- HIP kernels (gfx950) and the device half of the C ABI (include/vpt.h).
+ *
+ * render_kernel replaces main()'s OpenMP pixel loop (src/rt.cpp:767-805): one lane owns one
+ * pixel and runs its spp camera samples (src/rt.cpp:786-798) through the estimator, accumulating
+ * in FP64 in the reference's order, then writes the average (src/rt.cpp:800) once.  A wave
+ * covers an 8x8 pixel tile (neighbouring camera rays hit the same surfaces, which keeps the
+ * sphere loop and the shading branches coherent); a 256-thread workgroup covers 16x16.
+ */
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <string.h>
+
+#include "vpt_device.h"
+#include "vpt_internal.h"
+
+using namespace vpt;
+
+namespace {
+
+struct KParams {
+    int32_t w, h, spp, fb;
+    int32_t band_rows, band_stride, band_offset, shard_rows;
+    double sigma_a, sigma_s, g;
+    int32_t max_depth, est;
+    uint64_t seed;
+    double o[3], d[3], cx[3], cy[3];
+    void* out;
+    unsigned long long* counters;  /* counting mode: [tests, iterations] */
+};
+
+#define HIP_OK(expr)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return vpt_fail(VPT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));       \
+    } while (0)
+
+template <int EST, bool COUNT, int FB>
+__global__ __launch_bounds__(256) void render_kernel(KParams P, const DevScene* __restrict__ S)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (x >= P.w || lr >= P.shard_rows) return;
+    const int k = lr / P.band_rows, r = lr - k * P.band_rows;
+    const int fr = (P.band_offset + k * P.band_stride) * P.band_rows + r;  /* file row */
+    const int y = P.h - 1 - fr;                                              /* camera row */
+    const uint64_t idx = (uint64_t)fr * (uint64_t)P.w + (uint64_t)x;          /* src/rt.cpp:773 */
+    const Medium m{P.sigma_a, P.sigma_s, P.g, P.max_depth};
+    const dv3 o = mk(P.o[0], P.o[1], P.o[2]), cd = mk(P.d[0], P.d[1], P.d[2]);
+    const dv3 cx = mk(P.cx[0], P.cx[1], P.cx[2]), cy = mk(P.cy[0], P.cy[1], P.cy[2]);
+    dv3 acc = mk(0, 0, 0);
+    uint64_t tests = 0, iters = 0;
+    for (int i = 0; i < P.spp; ++i) {
+        Sampler<COUNT> smp;
+        smp.X = vpt_stream_start(P.seed, idx, (uint64_t)i);
+        smp.g = P.g;
+        smp.cnt.tests = 0;
+        smp.cnt.iterations = 0;
+        /* jittered camera ray, src/rt.cpp:787, x draw first */
+        double jx = smp.next();
+        double jy = smp.next();
+        dv3 dir = add(add(scl(cx, (((double)x + jx - 0.5) / P.w - .5)), scl(cy, (((double)y + jy - 0.5) / P.h - .5))), cd);
+        dir = nrm(dir);
+        dv3 L = trace_sample<EST, COUNT>(S, smp, o, dir, m);
+        acc = add(L, acc);
+        if (COUNT) {
+            tests += smp.cnt.tests;
+            iters += smp.cnt.iterations;
+        }
+    }
+    acc = scl(acc, (1 / (double)P.spp));
+    const size_t oi = ((size_t)lr * (size_t)P.w + (size_t)x) * 3;
+    if (FB == VPT_FB_F32) {
+        float* out = (float*)P.out;
+        out[oi] = (float)acc.x;
+        out[oi + 1] = (float)acc.y;
+        out[oi + 2] = (float)acc.z;
+    } else {
+        double* out = (double*)P.out;
+        out[oi] = acc.x;
+        out[oi + 1] = acc.y;
+        out[oi + 2] = acc.z;
+    }
+    if (COUNT) {
+        atomicAdd(&P.counters[0], (unsigned long long)tests);
+        atomicAdd(&P.counters[1], (unsigned long long)iters);
+    }
+}
+
+template <int EST>
+__global__ __launch_bounds__(256) void trace_batch_kernel(const vpt_ray* __restrict__ rays,
+                                                          const uint64_t* __restrict__ states, int n, Medium m,
+                                                          double g, const DevScene* __restrict__ S, double* out,
+                                                          uint64_t* out_states)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Sampler<false> smp;
+    smp.X = states[i] & 0xFFFFFFFFFFFFull;
+    smp.g = g;
+    dv3 L = trace_sample<EST, false>(S, smp, ld3(rays[i].o), ld3(rays[i].d), m);
+    out[3 * i] = L.x;
+    out[3 * i + 1] = L.y;
+    out[3 * i + 2] = L.z;
+    out_states[i] = smp.X;
+}
+
+__global__ void math_probe_kernel(int fn, const double* x, const double* y, double* out, int n)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double a = x[i], b = y[i], r = 0;
+    switch (fn) {
+    case 0: r = vm_sqrt(a); break;
+    case 1: r = vm_exp(a); break;
+    case 2: r = vm_log(a); break;
+    case 3: r = vm_sin(a); break;
+    case 4: r = vm_cos(a); break;
+    case 5: r = vm_tan(a); break;
+    case 6: r = vm_atan(a); break;
+    case 7: r = vm_acos(a); break;
+    case 8: r = vm_atan2(a, b); break;
+    default: r = a / b; break;
+    }
+    out[i] = r;
+}
+
+bool is_finite(double v) { return v == v && v - v == 0.0; }
+
+}  // namespace
+
+struct vpt_context {
+    int device;
+    DevScene* d_scene;
+    DevScene h_scene;
+    int has_scene;
+    unsigned long long* d_counters;
+};
+
+static int check_medium(const vpt_medium* m)
+{
+    if (!m) return vpt_fail(VPT_E_INVALID, "medium is NULL");
+    if (!is_finite(m->sigma_a) || !is_finite(m->sigma_s) || m->sigma_a < 0 || m->sigma_s < 0)
+        return vpt_fail(VPT_E_INVALID, "sigma_a/sigma_s must be finite and >= 0");
+    if (!is_finite(m->hg_g) || m->hg_g <= -1.0 || m->hg_g >= 1.0) return vpt_fail(VPT_E_INVALID, "hg_g must be in (-1, 1)");
+    if (m->max_depth < 0) return vpt_fail(VPT_E_INVALID, "max_depth must be >= 0");
+    if (m->estimator != VPT_FREE_FLIGHT && m->estimator != VPT_MIS_EQUIANGULAR)
+        return vpt_fail(VPT_E_INVALID, "unknown estimator %d", m->estimator);
+    return VPT_OK;
+}
+
+static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_out, KParams& K)
+{
+    if (!ctx || !p) return vpt_fail(VPT_E_INVALID, "NULL context or params");
+    if (!ctx->has_scene) return vpt_fail(VPT_E_INVALID, "no scene set (vpt_set_scene)");
+    if (p->width <= 0 || p->height <= 0 || p->spp <= 0) return vpt_fail(VPT_E_INVALID, "width/height/spp must be > 0");
+    if ((int64_t)p->width * p->height > (int64_t)1 << 31) return vpt_fail(VPT_E_INVALID, "image too large");
+    if (p->fb_format != VPT_FB_F32 && p->fb_format != VPT_FB_F64) return vpt_fail(VPT_E_INVALID, "bad fb_format");
+    int rc = check_medium(&p->medium);
+    if (rc) return rc;
+    int rows = vpt_shard_rows(p);
+    if (rows <= 0) return vpt_fail(VPT_E_INVALID, "bad band_rows/band_stride/band_offset or empty shard");
+    const double* cd = p->camera.d;
+    if (!is_finite(p->fov_scale) || !is_finite(cd[0]) || !is_finite(cd[1]) || !is_finite(cd[2]))
+        return vpt_fail(VPT_E_INVALID, "bad camera");
+    memset(&K, 0, sizeof K);
+    K.w = p->width;
+    K.h = p->height;
+    K.spp = p->spp;
+    K.fb = p->fb_format;
+    K.band_rows = p->band_rows;
+    K.band_stride = p->band_stride;
+    K.band_offset = p->band_offset;
+    K.shard_rows = rows;
+    K.sigma_a = p->medium.sigma_a;
+    K.sigma_s = p->medium.sigma_s;
+    K.g = p->medium.hg_g;
+    K.max_depth = p->medium.max_depth;
+    K.est = p->medium.estimator;
+    K.seed = p->seed;
+    for (int i = 0; i < 3; ++i) {
+        K.o[i] = p->camera.o[i];
+        K.d[i] = cd[i];
+    }
+    /* Vector cx = Vector(w * 0.5095 / h, 0., 0.); cy = (cx % camera.d).normalize() * 0.5095
+     * (src/rt.cpp:758-759), same operation order */
+    K.cx[0] = p->width * p->fov_scale / p->height;
+    K.cx[1] = 0.;
+    K.cx[2] = 0.;
+    double crx = K.cx[1] * cd[2] - K.cx[2] * cd[1];
+    double cry = K.cx[2] * cd[0] - K.cx[0] * cd[2];
+    double crz = K.cx[0] * cd[1] - K.cx[1] * cd[0];
+    double inv = 1.0 / sqrt(crx * crx + cry * cry + crz * crz);
+    K.cy[0] = crx * inv * p->fov_scale;
+    K.cy[1] = cry * inv * p->fov_scale;
+    K.cy[2] = crz * inv * p->fov_scale;
+    K.out = d_out;
+    return VPT_OK;
+}
+
+template <bool COUNT>
+static int launch_render(vpt_context* ctx, const KParams& K, hipStream_t stream)
+{
+    dim3 block(256);
+    dim3 grid((unsigned)((K.w + 15) / 16), (unsigned)((K.shard_rows + 15) / 16));
+    const DevScene* S = ctx->d_scene;
+    if (K.est == VPT_FREE_FLIGHT) {
+        if (K.fb == VPT_FB_F32) render_kernel<0, COUNT, VPT_FB_F32><<<grid, block, 0, stream>>>(K, S);
+        else render_kernel<0, COUNT, VPT_FB_F64><<<grid, block, 0, stream>>>(K, S);
+    } else {
+        if (K.fb == VPT_FB_F32) render_kernel<1, COUNT, VPT_FB_F32><<<grid, block, 0, stream>>>(K, S);
+        else render_kernel<1, COUNT, VPT_FB_F64><<<grid, block, 0, stream>>>(K, S);
+    }
+    HIP_OK(hipGetLastError());
+    return VPT_OK;
+}
+
+extern "C" {
+
+int vpt_context_create(int device, vpt_context** out)
+{
+    vpt_clear_error();
+    if (!out) return vpt_fail(VPT_E_INVALID, "vpt_context_create: out is NULL");
+    *out = nullptr;
+    int ndev = 0;
+    HIP_OK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return vpt_fail(VPT_E_INVALID, "vpt_context_create: device %d of %d", device, ndev);
+    HIP_OK(hipSetDevice(device));
+    vpt_context* c = new vpt_context();
+    memset(&c->h_scene, 0, sizeof c->h_scene);
+    c->device = device;
+    c->has_scene = 0;
+    c->d_scene = nullptr;
+    c->d_counters = nullptr;
+    hipError_t e = hipMalloc((void**)&c->d_scene, sizeof(DevScene));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 2 * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        vpt_context_destroy(c);
+        return vpt_fail(VPT_E_HIP, "vpt_context_create: hipMalloc: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return VPT_OK;
+}
+
+void vpt_context_destroy(vpt_context* ctx)
+{
+    if (!ctx) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->d_scene) (void)hipFree(ctx->d_scene);
+    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    (void)hipSetDevice(prev);
+    delete ctx;
+}
+
+int vpt_set_scene(vpt_context* ctx, const vpt_sphere* s, int n)
+{
+    vpt_clear_error();
+    if (!ctx || !s) return vpt_fail(VPT_E_INVALID, "vpt_set_scene: NULL argument");
+    if (n < 1) return vpt_fail(VPT_E_INVALID, "vpt_set_scene: empty scene");
+    if (n > VPT_MAX_SPHERES) return vpt_fail(VPT_E_TOO_MANY, "vpt_set_scene: %d spheres > %d", n, VPT_MAX_SPHERES);
+    DevScene h;
+    memset(&h, 0, sizeof h);
+    h.n = n;
+    for (int i = 0; i < n; ++i) {
+        const vpt_sphere& q = s[i];
+        if (q.material < 0 || q.material > 3)
+            return vpt_fail(VPT_E_UNSUPPORTED, "vpt_set_scene: sphere %d material %d", i, q.material);
+        const double* vals[6] = {q.p, q.c, q.radiance, q.eta, q.kappa, nullptr};
+        bool ok = is_finite(q.r) && q.r >= 0 && is_finite(q.alpha);
+        for (int a = 0; a < 5; ++a)
+            for (int c = 0; c < 3; ++c) ok = ok && is_finite(vals[a][c]);
+        if (!ok) return vpt_fail(VPT_E_INVALID, "vpt_set_scene: sphere %d has a non-finite or negative field", i);
+        h.sph[i] = q;
+        h.geo[i].px = q.p[0];
+        h.geo[i].py = q.p[1];
+        h.geo[i].pz = q.p[2];
+        h.geo[i].r2 = q.r * q.r;
+        h.geo[i].mat3 = q.material == 3;
+        h.geo[i].emitter = (q.radiance[0] > 0 || q.radiance[1] > 0 || q.radiance[2] > 0);
+        if (h.geo[i].emitter) h.emit[h.n_emit++] = i;
+        if (q.r > 0 && q.radiance[0] > 0) h.mis_light[h.n_mis++] = i;
+        if (q.material == 3) h.n_mat3++;
+    }
+    h.n_non3 = n - h.n_mat3;
+    HIP_OK(hipSetDevice(ctx->device));
+    HIP_OK(hipMemcpy(ctx->d_scene, &h, sizeof h, hipMemcpyHostToDevice));
+    ctx->h_scene = h;
+    ctx->has_scene = 1;
+    return VPT_OK;
+}
+
+int vpt_render_device(vpt_context* ctx, const vpt_params* p, void* d_out, void* stream)
+{
+    vpt_clear_error();
+    if (!d_out) return vpt_fail(VPT_E_INVALID, "vpt_render_device: d_out is NULL");
+    KParams K;
+    int rc = build_kparams(ctx, p, d_out, K);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(ctx->device));
+    return launch_render<false>(ctx, K, (hipStream_t)stream);
+}
+
+int vpt_render(vpt_context* ctx, const vpt_params* p, void* h_out)
+{
+    vpt_clear_error();
+    if (!h_out) return vpt_fail(VPT_E_INVALID, "vpt_render: h_out is NULL");
+    KParams K;
+    int rc = build_kparams(ctx, p, (void*)1, K);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(ctx->device));
+    size_t bytes = (size_t)K.shard_rows * (size_t)K.w * 3 * (K.fb == VPT_FB_F32 ? sizeof(float) : sizeof(double));
+    void* d = nullptr;
+    HIP_OK(hipMalloc(&d, bytes));
+    K.out = d;
+    rc = launch_render<false>(ctx, K, nullptr);
+    hipError_t e = rc ? hipSuccess : hipMemcpy(h_out, d, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (rc) return rc;
+    if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_render: %s", hipGetErrorString(e));
+    return VPT_OK;
+}
+
+int vpt_count_work(vpt_context* ctx, const vpt_params* p, uint64_t* tests, uint64_t* iterations)
+{
+    vpt_clear_error();
+    KParams K;
+    int rc = build_kparams(ctx, p, (void*)1, K);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(ctx->device));
+    size_t bytes = (size_t)K.shard_rows * (size_t)K.w * 3 * (K.fb == VPT_FB_F32 ? sizeof(float) : sizeof(double));
+    void* d = nullptr;
+    HIP_OK(hipMalloc(&d, bytes));
+    K.out = d;
+    K.counters = ctx->d_counters;
+    unsigned long long hc[2] = {0, 0};
+    hipError_t e = hipMemset(ctx->d_counters, 0, sizeof hc);
+    if (e == hipSuccess) {
+        rc = launch_render<true>(ctx, K, nullptr);
+        if (!rc) e = hipMemcpy(hc, ctx->d_counters, sizeof hc, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d);
+    if (rc) return rc;
+    if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_count_work: %s", hipGetErrorString(e));
+    if (tests) *tests = hc[0];
+    if (iterations) *iterations = hc[1];
+    return VPT_OK;
+}
+
+int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, const uint64_t* states, int n,
+                    double* out_rgb, uint64_t* out_states)
+{
+    vpt_clear_error();
+    if (!ctx || !rays || !states || !out_rgb || n < 0) return vpt_fail(VPT_E_INVALID, "vpt_trace_batch: bad arguments");
+    if (!ctx->has_scene) return vpt_fail(VPT_E_INVALID, "no scene set (vpt_set_scene)");
+    int rc = check_medium(m);
+    if (rc) return rc;
+    if (n == 0) return VPT_OK;
+    HIP_OK(hipSetDevice(ctx->device));
+    vpt_ray* dr = nullptr;
+    uint64_t *ds = nullptr, *dso = nullptr;
+    double* dout = nullptr;
+    hipError_t e = hipMalloc((void**)&dr, sizeof(vpt_ray) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc((void**)&ds, sizeof(uint64_t) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc((void**)&dso, sizeof(uint64_t) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * 3 * (size_t)n);
+    if (e == hipSuccess) e = hipMemcpy(dr, rays, sizeof(vpt_ray) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(ds, states, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        Medium mm{m->sigma_a, m->sigma_s, m->hg_g, m->max_depth};
+        dim3 grid((unsigned)((n + 255) / 256)), block(256);
+        if (m->estimator == VPT_FREE_FLIGHT)
+            trace_batch_kernel<0><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso);
+        else
+            trace_batch_kernel<1><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out_rgb, dout, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && out_states) e = hipMemcpy(out_states, dso, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(dr);
+    (void)hipFree(ds);
+    (void)hipFree(dso);
+    (void)hipFree(dout);
+    if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_trace_batch: %s", hipGetErrorString(e));
+    return VPT_OK;
+}
+
+int vpt_math_probe(vpt_context* ctx, int fn, const double* x, const double* y, double* out, int n)
+{
+    vpt_clear_error();
+    if (!ctx || !x || !y || !out || n < 0) return vpt_fail(VPT_E_INVALID, "vpt_math_probe: bad arguments");
+    if (n == 0) return VPT_OK;
+    HIP_OK(hipSetDevice(ctx->device));
+    double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    size_t b = sizeof(double) * (size_t)n;
+    hipError_t e = hipMalloc((void**)&dx, b);
+    if (e == hipSuccess) e = hipMalloc((void**)&dy, b);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, b);
+    if (e == hipSuccess) e = hipMemcpy(dx, x, b, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dy, y, b, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        math_probe_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256)>>>(fn, dx, dy, dout, n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, b, hipMemcpyDeviceToHost);
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+    (void)hipFree(dout);
+    if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_math_probe: %s", hipGetErrorString(e));
+    return VPT_OK;
+}
+
+}  // extern "C"

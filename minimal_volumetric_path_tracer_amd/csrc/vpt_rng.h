@@ -1,0 +1,54 @@
+/*
+ * vpt_rng.h -- per-sample random streams (host + device).
+ *
+ * The reference draws every number with libc erand48(seed) on ONE global state
+ * (include/Vector.h:38) shared by all OpenMP threads (src/rt.cpp:767) and seeded from 3 bytes of
+ * getentropy (src/rt.cpp:746): not reproducible, not shardable.  Here the generator is the same
+ * POSIX erand48 recurrence
+ *     X <- (0x5DEECE66D * X + 0xB) mod 2^48,   xi = X / 2^48,
+ * bit-identical to glibc's erand48 (which builds 1.m from X<<4 and subtracts 1.0), but every
+ * camera sample (pixel idx, sample i) owns a private 48-bit state derived from the image seed by
+ * two splitmix64 rounds.  Results therefore do not depend on thread, wave or GPU count.
+ * oracle/oracle_rng.h states the same spec independently; tests compare the two.
+ */
+#ifndef VPT_RNG_H
+#define VPT_RNG_H
+
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+#define VPT_HD __host__ __device__ static inline __attribute__((always_inline))
+#else
+#define VPT_HD static inline
+#endif
+
+VPT_HD uint64_t vpt_splitmix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* start state of sample `sample` of the pixel with file-order index `idx` (src/rt.cpp:773) */
+VPT_HD uint64_t vpt_stream_start(uint64_t seed, uint64_t idx, uint64_t sample)
+{
+    uint64_t k = vpt_splitmix64(seed + 0x9E3779B97F4A7C15ull * (idx + 1ull));
+    return vpt_splitmix64(k ^ (sample * 0xD1B54A32D192ED03ull + 1ull)) >> 16;
+}
+
+/* one erand48 draw: advances X, returns X/2^48 exactly (glibc erand48_r construction) */
+VPT_HD double vpt_erand48(uint64_t* X)
+{
+    uint64_t x = (*X * 0x5DEECE66Dull + 0xBull) & 0xFFFFFFFFFFFFull;
+    *X = x;
+    union {
+        uint64_t u;
+        double d;
+    } b;
+    b.u = 0x3FF0000000000000ull | (x << 4);
+    return b.d - 1.0;
+}
+
+#endif

@@ -1,0 +1,38 @@
+/*
+ * vpt_scene.h -- device-resident scene (host + device view).
+ *
+ * Replaces the reference's global std::vector<Sphere> spheres (include/Sphere.h:49,
+ * include/Sphere.cpp:7-107) and the per-iteration emitter scan of the estimators
+ * (include/vptShadeMethods.h:1293-1303, :1389-1407; include/misSamplingFunctions.h:106).
+ * Two views of each sphere: a 48-byte GeoSphere read by the intersection loop with a
+ * wave-uniform index (scalar loads), and the 144-byte reference record for shading lookups by a
+ * per-lane id.  Derived lists are computed once per scene on the host.
+ */
+#ifndef VPT_SCENE_H
+#define VPT_SCENE_H
+
+#include <stdint.h>
+#include "../../include/vpt.h"
+
+struct GeoSphere {
+    double px, py, pz;  /* centre */
+    double r2;          /* fl(r*r), exactly the product Sphere::intersect forms (Sphere.h:30) */
+    int32_t mat3;       /* material == 3 (skipped by intersectVPT) */
+    int32_t emitter;    /* any radiance channel > 0 (vptShadeMethods.h:1296) */
+    int32_t pad_[2];
+};
+
+struct DevScene {
+    int32_t n;          /* number of spheres */
+    int32_t n_emit;     /* emitters (idsource candidates) */
+    int32_t n_mis;      /* spheres with r > 0 && radiance.x > 0 (MISv2 light loop) */
+    int32_t n_mat3;     /* material-3 spheres */
+    int32_t n_non3;     /* n - n_mat3 */
+    int32_t pad_[3];
+    int32_t emit[VPT_MAX_SPHERES];
+    int32_t mis_light[VPT_MAX_SPHERES];
+    GeoSphere geo[VPT_MAX_SPHERES];
+    vpt_sphere sph[VPT_MAX_SPHERES];
+};
+
+#endif

@@ -1,0 +1,72 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TESTS = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(TESTS, "golden")
+for p in (ROOT, TESTS):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libvpt.so on the device)")
+    config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+def _ensure_built():
+    need = [
+        os.path.join(ROOT, "oracle", "liboracle.so"),
+        os.path.join(ROOT, "oracle", "liboracle_vm.so"),
+        os.path.join(ROOT, "minimal_volumetric_path_tracer_amd", "libvpt.so"),
+    ]
+    if not all(os.path.exists(p) for p in need):
+        import __graft_entry__
+
+        __graft_entry__.build()
+
+
+_ensure_built()
+
+
+@pytest.fixture(scope="session")
+def samples():
+    return dict(np.load(os.path.join(GOLDEN, "samples.npz")))
+
+
+@pytest.fixture(scope="session")
+def prims():
+    return dict(np.load(os.path.join(GOLDEN, "primitives.npz")))
+
+
+@pytest.fixture(scope="session")
+def orc():
+    from oracle.oracle import Oracle
+
+    return Oracle(portable=False)
+
+
+@pytest.fixture(scope="session")
+def orc_vm():
+    from oracle.oracle import Oracle
+
+    return Oracle(portable=True)
+
+
+@pytest.fixture(scope="session")
+def gpu_tracer():
+    from minimal_volumetric_path_tracer_amd import Tracer
+
+    t = Tracer(0)
+    yield t
+    t.close()
+
+
+def bitwise_equal(a, b):
+    """elementwise identical bits, NaN == NaN (any payload), -0.0 == +0.0 only when both zero"""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    return (a == b) | (np.isnan(a) & np.isnan(b))

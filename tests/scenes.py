@@ -1,0 +1,97 @@
+"""Scenes used by the parity fixtures and tests (numpy records with the reference Sphere layout,
+include/Sphere.h:12-21, 144 bytes).  `default` is include/Sphere.cpp:11-22; the others widen
+coverage to branches the default scene never takes."""
+import numpy as np
+
+SPHERE_DTYPE = np.dtype(
+    {
+        "names": ["r", "p", "c", "radiance", "material", "reserved_", "eta", "kappa", "alpha"],
+        "formats": ["<f8", ("<f8", 3), ("<f8", 3), ("<f8", 3), "<i4", "<i4", ("<f8", 3), ("<f8", 3), "<f8"],
+        "offsets": [0, 8, 32, 56, 80, 84, 88, 112, 136],
+        "itemsize": 144,
+    }
+)
+
+AL_ETA = (1.66058, 0.88143, 0.521467)
+AL_KAPPA = (9.2282, 6.27077, 4.83803)
+
+
+def sph(r, p, c=(0, 0, 0), rad=(0, 0, 0), mat=0, eta=(0, 0, 0), kappa=(0, 0, 0), alpha=0.0):
+    s = np.zeros(1, dtype=SPHERE_DTYPE)
+    s["r"], s["p"], s["c"], s["radiance"], s["material"] = r, p, c, rad, mat
+    s["eta"], s["kappa"], s["alpha"] = eta, kappa, alpha
+    return s
+
+
+def walls(left=(.5, .5, .5), right=(.0, .0, .5)):
+    return [
+        sph(1e5, (-1e5 - 49, 0, 0), left),
+        sph(1e5, (1e5 + 49, 0, 0), right),
+        sph(1e5, (0, 0, -1e5 - 81.6), (.5, .5, .5)),
+        sph(1e5, (0, -1e5 - 40.8, 0), (.5, .5, .5)),
+        sph(1e5, (0, 1e5 + 40.8, 0), (.5, .5, .5)),
+    ]
+
+
+def default_scene():
+    return np.concatenate(walls() + [
+        sph(16.5, (-23, -24.3, -34.6), mat=1, eta=AL_ETA, kappa=AL_KAPPA, alpha=0.09),
+        sph(16.5, (23, -24.3, -3.6), (.0, .0, .9)),
+        sph(2, (0, 24.3, -35), rad=(100, 100, 0)),
+        sph(0, (-23, 24.3, 0), rad=(6000, 0, 0)),
+        sph(2, (23, 24.3, 35), rad=(75, 75, 60)),
+    ])
+
+
+def dielectric_scene():
+    """blue Lambert sphere replaced by a smooth dielectric (material 2, eta 1.5 hard-coded)."""
+    s = default_scene()
+    s[6]["material"] = 2
+    s[6]["c"] = (.9, .9, .9)
+    return s
+
+
+def mat3_scene():
+    """a material-3 ("volumetric") sphere around the point light: shadow rays fall back to
+    visibilityVPT + multipleT (include/vptShadeMethods.h:68-72)."""
+    return np.concatenate([default_scene(), sph(4.0, (-23, 24.3, 0), (.5, .5, .5), mat=3)])
+
+
+def point_lights_scene():
+    """only point lights: the MISv2 light loop is empty (include/misSamplingFunctions.h:106)."""
+    return np.concatenate(walls() + [
+        sph(16.5, (-23, -24.3, -34.6), mat=1, eta=AL_ETA, kappa=AL_KAPPA, alpha=0.3),
+        sph(16.5, (23, -24.3, -3.6), (.7, .6, .2)),
+        sph(0, (-23, 24.3, 0), rad=(3000, 3000, 1000)),
+        sph(0, (20, 10, -40), rad=(1000, 2000, 4000)),
+    ])
+
+
+def no_emitter_scene():
+    s = default_scene()
+    return np.concatenate([s[:7]])
+
+
+SCENES = {
+    "default": default_scene,
+    "dielectric": dielectric_scene,
+    "mat3": mat3_scene,
+    "point_lights": point_lights_scene,
+    "no_emitter": no_emitter_scene,
+}
+
+
+# independent (pure Python) statement of the per-sample stream spec (csrc/vpt_rng.h)
+M64 = (1 << 64) - 1
+
+
+def splitmix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def stream_state(seed, idx, sample):
+    k = splitmix64((seed + 0x9E3779B97F4A7C15 * (idx + 1)) & M64)
+    return splitmix64(k ^ ((sample * 0xD1B54A32D192ED03 + 1) & M64)) >> 16

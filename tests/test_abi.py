@@ -1,0 +1,116 @@
+"""C ABI checks that need no GPU: libvpt.so loads and exports every function include/vpt.h
+declares, the structs have the reference's layout, host-side helpers (defaults, sharding,
+stream keys, PPM encoding) match the reference and the oracle."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+from conftest import GOLDEN, ROOT
+from scenes import SCENES, stream_state
+
+import minimal_volumetric_path_tracer_amd as vpt
+from minimal_volumetric_path_tracer_amd import _lib
+
+
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "vpt.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vpt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol():
+    names = _header_functions()
+    assert len(names) >= 15
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert hasattr(L, n), n
+    bound = {p[0] for p in _lib.PROTOTYPES}
+    assert bound == set(names), set(names) ^ bound
+    assert vpt.lib().vpt_abi_version() == 1
+
+
+def test_struct_layouts():
+    assert vpt.SPHERE_DTYPE.itemsize == 144
+    offs = {k: v[1] for k, v in vpt.SPHERE_DTYPE.fields.items()}
+    assert offs == {"r": 0, "p": 8, "c": 32, "radiance": 56, "material": 80, "reserved_": 84, "eta": 88,
+                    "kappa": 112, "alpha": 136}
+    assert ctypes.sizeof(_lib.vpt_ray) == 48
+    assert ctypes.sizeof(_lib.vpt_medium) == 32
+    assert ctypes.sizeof(_lib.vpt_params) == 16 + 32 + 8 + 48 + 8 + 16
+
+
+def test_default_scene_is_reference_scene():
+    ref = np.load(os.path.join(GOLDEN, "default_scene.npy"))
+    assert np.array_equal(vpt.default_scene().view(np.uint8), ref)
+
+
+def test_default_params_are_reference_main():
+    p = _lib.vpt_params()
+    vpt.lib().vpt_default_params(ctypes.byref(p))
+    assert (p.width, p.height, p.spp) == (1024, 768, 16)
+    assert (p.medium.sigma_a, p.medium.sigma_s, p.medium.hg_g, p.medium.max_depth) == (0.001, 0.009, 0.0, 0)
+    assert list(p.camera.o) == [0, 11.2, 214]
+    d = np.array([0, -0.042612, -1.0])
+    inv = 1.0 / np.sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2])
+    assert list(p.camera.d) == list(d * inv)
+    assert p.fov_scale == 0.5095
+
+
+def test_stream_state_matches_spec(orc):
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        s, i, k = (int(x) for x in (rng.integers(0, 2**63), rng.integers(0, 2**24), rng.integers(0, 2**16)))
+        assert vpt.stream_state(s, i, k) == stream_state(s, i, k) == orc.stream_state(s, i, k)
+
+
+@pytest.mark.parametrize("h,band,stride", [(40, 8, 2), (40, 5, 3), (1024, 16, 8), (7, 3, 4), (768, 768, 1)])
+def test_shard_rows(h, band, stride):
+    tot = 0
+    for off in range(stride):
+        cfg = vpt.RenderConfig(width=4, height=h, band_rows=band, band_stride=stride, band_offset=off)
+        rows = [fr for b in range(off, (h + band - 1) // band, stride) for fr in range(b * band, min(h, (b + 1) * band))]
+        assert cfg.shard_rows() == len(rows)
+        tot += len(rows)
+    assert tot == h
+
+
+def test_ppm_bytes_match_reference_writer(orc, tmp_path):
+    rng = np.random.default_rng(3)
+    fb = rng.normal(0.2, 0.6, (37, 53, 3))
+    fb[0, 0] = [np.nan, np.inf, -np.inf]
+    fb[1, :4, 0] = [0.0, 1.0, -0.0, 1.0 + 1e-16]
+    a = tmp_path / "a.ppm"
+    b = tmp_path / "b.ppm"
+    vpt.write_ppm(str(a), fb)
+    orc.write_ppm(str(b), fb)
+    assert a.read_bytes() == b.read_bytes() == vpt.encode_ppm(fb)
+    # float32 framebuffers are written from their float values
+    f32 = fb.astype(np.float32)
+    orc.write_ppm(str(b), f32.astype(np.float64))
+    assert vpt.encode_ppm(f32) == b.read_bytes()
+
+
+def test_ppm_format_of_reference_program():
+    facts = json.load(open(os.path.join(GOLDEN, "reference_ppm.json")))["program"]
+    fb = np.full((768, 1024, 3), 0.25)
+    data = vpt.encode_ppm(fb)
+    assert data.startswith(facts["header"].encode())
+    assert data.endswith(b" ") == facts["ends_with_space"] and data.endswith(b"\n") == facts["ends_with_newline"]
+    assert len(data.split()) - 4 == facts["n_values"]
+
+
+def test_large_ppm_parallel_encoder_matches(orc, tmp_path):
+    rng = np.random.default_rng(4)
+    fb = rng.uniform(-0.1, 1.2, (300, 400, 3))
+    b = tmp_path / "b.ppm"
+    orc.write_ppm(str(b), fb)
+    assert vpt.encode_ppm(fb) == b.read_bytes()
+
+
+def test_scene_constructors():
+    s = vpt.scene(vpt.Sphere(1.0, (0, 0, 0), radiance=(1, 2, 3)), vpt.Sphere(2.0, (1, 2, 3), material=1, alpha=0.1))
+    assert s.dtype == vpt.SPHERE_DTYPE and len(s) == 2
+    assert np.array_equal(vpt.default_scene().view(np.uint8), SCENES["default"]().view(np.uint8))
