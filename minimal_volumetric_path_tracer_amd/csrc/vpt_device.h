@@ -654,101 +654,152 @@ VPT_DEV double equiangular_params2(const DevScene* __restrict__ S, Sampler<COUNT
 VPT_DEV double equiangular_prob(double D, double ta, double tb, double s) { return D / vm_fabs(tb - ta) / (s * s + D * D); }
 
 /* ------------------------------------------------------------------ estimators */
+/* iterativeVPTracerFree (EST = 0), include/vptShadeMethods.h:1263-1340, and
+ * MISVPTTracerRecursive (EST = 1), :1345-1481, split into the pieces a wave schedules
+ * separately: decide() = one loop iteration up to the event choice (intersection, light pick,
+ * distance sample), then surface_event() or medium_event().  The reference's FF stack holds at
+ * most one frame and its MIS recursion is linear, so a path is (ray, throughput, radiance, depth)
+ * carried forward. */
 struct Medium {
     double sigma_a, sigma_s, g;
     int max_depth;
 };
 
-/* iterativeVPTracerFree (EST = 0), include/vptShadeMethods.h:1263-1340, and
- * MISVPTTracerRecursive (EST = 1), :1345-1481, as one forward loop with a running throughput
- * (the reference's FF stack holds at most one frame; the MIS recursion is linear). */
-template <int EST, bool COUNT>
-__device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, const Medium& m)
+struct Path {
+    dv3 o, d;      /* current ray */
+    dv3 beta;      /* throughput */
+    dv3 L;         /* radiance gathered so far */
+    int depth;     /* loop iteration (the reference's `profundidad`) */
+};
+
+struct Event {
+    double t;      /* surface distance (MAXFLOAT when the ray escapes) */
+    double dist;   /* FF: free-flight distance; MIS: equi-angular distance d_final */
+    double pdf;    /* MIS: equi-angular pdf * (1 - psurf) */
+    int id;        /* surface sphere */
+    int src;       /* light picked for next-event estimation */
+};
+
+enum { EV_END = 0, EV_SURF = 1, EV_MED = 2 };
+
+/* Russian roulette at the top of a loop iteration (vptShadeMethods.h:1282 / :1354) and the depth
+ * cap extension; true = the path continues. */
+template <bool COUNT>
+VPT_DEV bool continue_path(Sampler<COUNT>& smp, const Path& p, const Medium& m)
 {
-    dv3 beta = mk(1, 1, 1);
-    dv3 L = mk(0, 0, 0);
+    if (m.max_depth > 0 && p.depth >= m.max_depth) return false;
+    if (COUNT) smp.cnt.iterations++;
+    const double q = 1 - 0.6;
+    return !(smp.next() < q);
+}
+
+/* vptShadeMethods.h:1284-1307 (FF) / :1357-1426 (MIS): what happens to the path this iteration. */
+template <int EST, bool COUNT>
+VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, Event& e, const Medium& m)
+{
+    const double sigma_t = m.sigma_a + m.sigma_s;
+    int id = 0;
+    double t;
+    if (!scene_intersect(S, smp, p.o, p.d, t, id, false)) t = VPT_MAXFLOAT;
+    const int count = S->n_emit;
+    if (count == 0) return EV_END;
+    e.t = t;
+    e.id = id;
+    e.src = S->emit[(int)(smp.next() * count)];
+    bool surf;
+    if (EST == 0) {
+        e.dist = -vm_log(1 - smp.next()) / sigma_t;  /* freeFlightSample, vptSamplingFunctions.h:11-14 */
+        surf = e.dist > t;
+    } else {
+        double D = 0, ta = 0, tb = 0, sd = 0;
+        double psurf = vm_exp(sigma_t * t * -1.0);
+        e.dist = equiangular_params2(S, smp, e.src, t, p.o, p.d, D, ta, tb, sd);
+        e.pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
+        surf = smp.next() < psurf;
+    }
+    if (!surf) return EV_MED;
+    if (S->geo[id].emitter) {  /* the path ends on a light; only a camera ray sees it */
+        if (p.depth == 0) p.L = EST == 0 ? mul(sph_rad(S, id), p.beta) : sph_rad(S, id);
+        return EV_END;
+    }
+    return EV_SURF;
+}
+
+/* surface event: point-light NEE (pLight), sphere-light MIS (MISv2), BSDF continuation (bdsf) */
+template <int EST, bool COUNT>
+VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
+                           const Medium& m)
+{
+    const double sigma_t = m.sigma_a + m.sigma_s;
+    const double continueprob = 0.6;
+    const double probSource = 1.0 / S->n_emit;
+    const int id = e.id, src = e.src;
+    const dv3 xs = add(p.o, scl(p.d, e.t));
+    const dv3 nx = nrm(sub(xs, sph_p(S, id)));
+    const double alpha = S->sph[id].alpha;
+    double Trs = transmitance(xs, sph_p(S, src), sigma_t);
+    dv3 Ldp = scl(scl(p_light(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+    dv3 Ld = mis_v2(S, smp, id, xs, nx, p.d, alpha, sigma_t);
+    dv3 wi = mk(0, 0, 0);
+    double pdf = 0;
+    dv3 fs = bdsf(S, smp, wi, p.d, nx, pdf, id);
+    wi = nrm(wi);
+    double cosine = dot(nx, wi);
+    if (EST == 0) p.L = add(p.L, scl(mul(add(Ldp, Ld), p.beta), (1 / continueprob)));
+    else p.L = add(p.L, mul(p.beta, scl(add(Ldp, Ld), (1 / continueprob))));
+    p.beta = scl(scl(scl(mul(p.beta, fs), (1 / continueprob)), cosine), (1 / pdf));
+    p.o = xs;
+    p.d = wi;
+    p.depth++;
+}
+
+/* medium event: single-scattering NEE toward the picked light, phase-function continuation */
+template <int EST, bool COUNT>
+VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
+                          const Medium& m)
+{
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
     const double continueprob = 0.6;
-    const double q = 1 - continueprob;
-    const int count = S->n_emit;
-    for (int depth = 0;; ++depth) {
-        if (m.max_depth > 0 && depth >= m.max_depth) break;
-        if (COUNT) smp.cnt.iterations++;
-        if (smp.next() < q) break;
-        double t;
-        int id = 0;
-        if (!scene_intersect(S, smp, o, d, t, id, false)) t = VPT_MAXFLOAT;
-        dv3 xs = add(o, scl(d, t));
-        dv3 nx = nrm(sub(xs, sph_p(S, id)));
-        if (count == 0) break;
-        double probSource = 1.0 / count;
-        int idsource = S->emit[(int)(smp.next() * count)];
-        if (EST == 0) {
-            double dist = -vm_log(1 - smp.next()) / sigma_t;  /* freeFlightSample, vptSamplingFunctions.h:11-14 */
-            if (dist > t) {
-                if (S->geo[id].emitter) {
-                    if (depth == 0) L = mul(sph_rad(S, id), beta);
-                    break;
-                }
-                double alpha = S->sph[id].alpha;
-                double Trs = transmitance(xs, sph_p(S, idsource), sigma_t);
-                dv3 Ldp = scl(scl(p_light(S, smp, id, xs, nx, d, idsource, alpha), Trs), (1 / probSource));
-                dv3 Ld = mis_v2(S, smp, id, xs, nx, d, alpha, sigma_t);
-                dv3 wi = mk(0, 0, 0);
-                double pdf = 0;
-                dv3 fs = bdsf(S, smp, wi, d, nx, pdf, id);
-                wi = nrm(wi);
-                double cosine = dot(nx, wi);
-                L = add(L, scl(mul(add(Ldp, Ld), beta), (1 / continueprob)));
-                beta = scl(scl(scl(mul(beta, fs), (1 / continueprob)), cosine), (1 / pdf));
-                o = xs;
-                d = wi;
-            } else {
-                dv3 xt = add(o, scl(d, dist));
-                dv3 Ld = single_scattering(S, smp, xt, d, idsource, sigma_t, false, sigma_s, 1.0, probSource);
-                dv3 wi = phase_sample(smp, d);
-                L = add(L, scl(scl(mul(Ld, beta), (sigma_s / sigma_t)), (1 / continueprob)));
-                beta = scl(scl(beta, (sigma_s / sigma_t)), (1 / continueprob));
-                o = xt;
-                d = wi;
-            }
-        } else {
-            double D = 0, ta = 0, tb = 0, sd = 0;
-            double psurf = vm_exp(sigma_t * t * -1.0);
-            double d_final = equiangular_params2(S, smp, idsource, t, o, d, D, ta, tb, sd);
-            double pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
-            if (smp.next() < psurf) {
-                if (S->geo[id].emitter) {
-                    if (depth == 0) L = sph_rad(S, id);
-                    break;
-                }
-                double alpha = S->sph[id].alpha;
-                double Trs = transmitance(xs, sph_p(S, idsource), sigma_t);
-                dv3 Ldp = scl(scl(p_light(S, smp, id, xs, nx, d, idsource, alpha), Trs), (1 / probSource));
-                dv3 Ld = mis_v2(S, smp, id, xs, nx, d, alpha, sigma_t);
-                dv3 wi = mk(0, 0, 0);
-                double spdf = 0;
-                dv3 fs = bdsf(S, smp, wi, d, nx, spdf, id);
-                wi = nrm(wi);
-                double cosine = dot(nx, wi);
-                L = add(L, mul(beta, scl(add(Ldp, Ld), (1 / continueprob))));
-                beta = scl(scl(scl(mul(beta, fs), (1 / continueprob)), cosine), (1 / spdf));
-                o = xs;
-                d = wi;
-            } else {
-                dv3 xt = add(o, scl(d, d_final));
-                double T = transmitance(o, xt, sigma_t);
-                dv3 Ld = single_scattering(S, smp, xt, d, idsource, sigma_t, true, sigma_s, T, probSource);
-                dv3 wi = phase_sample(smp, d);
-                L = add(L, mul(beta, scl(scl(Ld, (1 / pdf)), (1 / continueprob))));
-                beta = scl(scl(scl(scl(beta, sigma_s), T), (1 / continueprob)), (1 / pdf));
-                o = xt;
-                d = wi;
-            }
-        }
+    const double probSource = 1.0 / S->n_emit;
+    dv3 xt = add(p.o, scl(p.d, e.dist));
+    if (EST == 0) {
+        dv3 Ld = single_scattering(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
+        dv3 wi = phase_sample(smp, p.d);
+        p.L = add(p.L, scl(scl(mul(Ld, p.beta), (sigma_s / sigma_t)), (1 / continueprob)));
+        p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
+        p.d = wi;
+    } else {
+        double T = transmitance(p.o, xt, sigma_t);
+        dv3 Ld = single_scattering(S, smp, xt, p.d, e.src, sigma_t, true, sigma_s, T, probSource);
+        dv3 wi = phase_sample(smp, p.d);
+        p.L = add(p.L, mul(p.beta, scl(scl(Ld, (1 / e.pdf)), (1 / continueprob))));
+        p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / e.pdf));
+        p.d = wi;
     }
-    return L;
+    p.o = xt;
+    p.depth++;
+}
+
+/* One camera sample, sequentially (the reference's per-sample call; used by vpt_trace_batch). */
+template <int EST, bool COUNT>
+__device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, const Medium& m)
+{
+    Path p;
+    p.o = o;
+    p.d = d;
+    p.beta = mk(1, 1, 1);
+    p.L = mk(0, 0, 0);
+    p.depth = 0;
+    Event e;
+    e.pdf = 0;
+    while (continue_path(smp, p, m)) {
+        int ev = decide<EST>(S, smp, p, e, m);
+        if (ev == EV_END) break;
+        if (ev == EV_SURF) surface_event<EST>(S, smp, p, e, m);
+        else medium_event<EST>(S, smp, p, e, m);
+    }
+    return p.L;
 }
 
 }  // namespace vpt

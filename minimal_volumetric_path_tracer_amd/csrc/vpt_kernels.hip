@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "vpt_device.h"
@@ -28,6 +29,9 @@ struct KParams {
     double o[3], d[3], cx[3], cy[3];
     void* out;
     unsigned long long* counters;  /* counting mode: [tests, iterations] */
+    unsigned* queue;               /* pixel work queue head (zeroed before each launch) */
+    int32_t tiles_x, tiles_y;      /* 8x8 pixel tiles covering the shard */
+    int32_t cost_surf, cost_med;   /* event scheduler weights */
 };
 
 #define HIP_OK(expr)                                                                         \
@@ -38,7 +42,7 @@ struct KParams {
     } while (0)
 
 template <int EST, bool COUNT, int FB>
-__global__ __launch_bounds__(256) void render_kernel(KParams P, const DevScene* __restrict__ S)
+__global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const DevScene* __restrict__ S)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -90,6 +94,159 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P, const DevScene* 
     }
 }
 
+/* camera ray of one sample, src/rt.cpp:787 (x draw first) */
+template <bool COUNT>
+__device__ __forceinline__ dv3 camera_dir(const KParams& P, Sampler<COUNT>& smp, int x, int y)
+{
+    const dv3 cd = mk(P.d[0], P.d[1], P.d[2]);
+    const dv3 cx = mk(P.cx[0], P.cx[1], P.cx[2]), cy = mk(P.cy[0], P.cy[1], P.cy[2]);
+    double jx = smp.next();
+    double jy = smp.next();
+    dv3 dir = add(add(scl(cx, (((double)x + jx - 0.5) / P.w - .5)), scl(cy, (((double)y + jy - 0.5) / P.h - .5))), cd);
+    return nrm(dir);
+}
+
+template <int FB>
+__device__ __forceinline__ void store_pixel(const KParams& P, int x, int lr, dv3 acc)
+{
+    acc = scl(acc, (1 / (double)P.spp));  /* src/rt.cpp:800 */
+    const size_t oi = ((size_t)lr * (size_t)P.w + (size_t)x) * 3;
+    if (FB == VPT_FB_F32) {
+        float* out = (float*)P.out;
+        out[oi] = (float)acc.x;
+        out[oi + 1] = (float)acc.y;
+        out[oi + 2] = (float)acc.z;
+    } else {
+        double* out = (double*)P.out;
+        out[oi] = acc.x;
+        out[oi + 1] = acc.y;
+        out[oi + 2] = acc.z;
+    }
+}
+
+/*
+ * Persistent wavefront scheduler.  Every lane owns one pixel at a time and runs that pixel's
+ * camera samples strictly in order (so the per-pixel FP64 sum is the reference's, bit for bit),
+ * but the wave no longer waits for its longest path:
+ *   - path regeneration: a lane whose path ends starts its next sample at once;
+ *   - a lane that finishes its pixel takes the next one from a device-wide queue (one atomic per
+ *     wave, 8x8-tile order for coherent camera rays), so waves drain together at the very end;
+ *   - deferred events: after the common part of an iteration (roulette, intersection, light and
+ *     distance sampling) a lane holds a pending SURFACE or MEDIUM event; each round the wave runs
+ *     only ONE of the two shading blocks -- the one with more lanes per unit of cost -- and the
+ *     other lanes keep their event for a later round (no data moves, no divergence between the
+ *     two blocks).
+ */
+template <int EST, bool COUNT, int FB>
+__global__ __launch_bounds__(256) void render_kernel(KParams P, const DevScene* __restrict__ S)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
+    const Medium m{P.sigma_a, P.sigma_s, P.g, P.max_depth};
+    const dv3 o0 = mk(P.o[0], P.o[1], P.o[2]);
+    const unsigned npix = (unsigned)P.tiles_x * (unsigned)P.tiles_y * 64u;
+
+    int x = 0, y = 0, lr = 0;
+    uint64_t idx = 0;
+    int i = 0;                 /* next sample to start */
+    bool done = false, need_pixel = true, in_path = false;
+    int pending = EV_END;
+    dv3 acc = mk(0, 0, 0);
+    Path p;
+    Event e;
+    e.pdf = 0;
+    Sampler<COUNT> smp;
+    smp.X = 0;
+    smp.g = P.g;
+    smp.cnt.tests = 0;
+    smp.cnt.iterations = 0;
+
+    while (true) {
+        /* (1) converged: lanes without a pixel take the next ones from the queue */
+        const uint64_t needm = __ballot(need_pixel && !done);
+        if (needm) {
+            const int leader = __ffsll((unsigned long long)needm) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(P.queue, (unsigned)__popcll(needm));
+            base = __shfl(base, leader);
+            if (need_pixel && !done) {
+                const unsigned q = base + (unsigned)__popcll(needm & below);
+                if (q >= npix) {
+                    done = true;
+                } else {
+                    const unsigned tile = q >> 6, within = q & 63u;
+                    x = (int)(tile % (unsigned)P.tiles_x) * 8 + (int)(within & 7u);
+                    lr = (int)(tile / (unsigned)P.tiles_x) * 8 + (int)(within >> 3);
+                    if (x < P.w && lr < P.shard_rows) {
+                        const int k = lr / P.band_rows, r = lr - k * P.band_rows;
+                        const int fr = (P.band_offset + k * P.band_stride) * P.band_rows + r; /* file row */
+                        y = P.h - 1 - fr;                                                       /* camera row */
+                        idx = (uint64_t)fr * (uint64_t)P.w + (uint64_t)x;                       /* src/rt.cpp:773 */
+                        i = 0;
+                        acc = mk(0, 0, 0);
+                        need_pixel = false;
+                    }
+                }
+            }
+        }
+        if (__ballot(!done) == 0) break;
+
+        /* (2) lanes without a pending event advance their path to the next event */
+        if (!done && !need_pixel && pending == EV_END) {
+            while (true) {
+                if (!in_path) {
+                    if (i == P.spp) {
+                        store_pixel<FB>(P, x, lr, acc);
+                        need_pixel = true;
+                        break;
+                    }
+                    smp.X = vpt_stream_start(P.seed, idx, (uint64_t)i);
+                    ++i;
+                    p.o = o0;
+                    p.d = camera_dir(P, smp, x, y);
+                    p.beta = mk(1, 1, 1);
+                    p.L = mk(0, 0, 0);
+                    p.depth = 0;
+                    in_path = true;
+                }
+                if (!continue_path(smp, p, m)) {
+                    acc = add(p.L, acc);  /* src/rt.cpp:794 */
+                    in_path = false;
+                    continue;
+                }
+                const int ev = decide<EST>(S, smp, p, e, m);
+                if (ev == EV_END) {
+                    acc = add(p.L, acc);
+                    in_path = false;
+                    continue;
+                }
+                pending = ev;
+                break;
+            }
+        }
+
+        /* (3) run one shading block: the one with more pending lanes per unit of cost */
+        const int ns = __popcll(__ballot(pending == EV_SURF));
+        const int nm = __popcll(__ballot(pending == EV_MED));
+        if (ns + nm == 0) continue;
+        if (ns * P.cost_med >= nm * P.cost_surf) {
+            if (pending == EV_SURF) {
+                surface_event<EST>(S, smp, p, e, m);
+                pending = EV_END;
+            }
+        } else {
+            if (pending == EV_MED) {
+                medium_event<EST>(S, smp, p, e, m);
+                pending = EV_END;
+            }
+        }
+    }
+    if (COUNT) {
+        atomicAdd(&P.counters[0], (unsigned long long)smp.cnt.tests);
+        atomicAdd(&P.counters[1], (unsigned long long)smp.cnt.iterations);
+    }
+}
+
 template <int EST>
 __global__ __launch_bounds__(256) void trace_batch_kernel(const vpt_ray* __restrict__ rays,
                                                           const uint64_t* __restrict__ states, int n, Medium m,
@@ -138,6 +295,7 @@ struct vpt_context {
     DevScene h_scene;
     int has_scene;
     unsigned long long* d_counters;
+    unsigned* d_queue;
 };
 
 static int check_medium(const vpt_medium* m)
@@ -161,8 +319,9 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
     if (p->fb_format != VPT_FB_F32 && p->fb_format != VPT_FB_F64) return vpt_fail(VPT_E_INVALID, "bad fb_format");
     int rc = check_medium(&p->medium);
     if (rc) return rc;
-    int rows = vpt_shard_rows(p);
-    if (rows <= 0) return vpt_fail(VPT_E_INVALID, "bad band_rows/band_stride/band_offset or empty shard");
+    if (p->band_rows <= 0 || p->band_stride <= 0 || p->band_offset < 0 || p->band_offset >= p->band_stride)
+        return vpt_fail(VPT_E_INVALID, "bad band_rows/band_stride/band_offset");
+    int rows = vpt_shard_rows(p);  /* 0: more shards than bands -- a legal no-op */
     const double* cd = p->camera.d;
     if (!is_finite(p->fov_scale) || !is_finite(cd[0]) || !is_finite(cd[1]) || !is_finite(cd[2]))
         return vpt_fail(VPT_E_INVALID, "bad camera");
@@ -201,21 +360,61 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
     return VPT_OK;
 }
 
-template <bool COUNT>
-static int launch_render(vpt_context* ctx, const KParams& K, hipStream_t stream)
+template <typename Kern>
+static int persistent_grid(vpt_context* ctx, Kern kern, int* blocks)
 {
-    dim3 block(256);
-    dim3 grid((unsigned)((K.w + 15) / 16), (unsigned)((K.shard_rows + 15) / 16));
+    int per_cu = 0, cus = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
+    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    if (per_cu < 1) per_cu = 1;
+    *blocks = per_cu * cus;
+    return VPT_OK;
+}
+
+static int env_int(const char* name, int dflt)
+{
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+template <int EST, bool COUNT, int FB>
+static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
+{
     const DevScene* S = ctx->d_scene;
-    if (K.est == VPT_FREE_FLIGHT) {
-        if (K.fb == VPT_FB_F32) render_kernel<0, COUNT, VPT_FB_F32><<<grid, block, 0, stream>>>(K, S);
-        else render_kernel<0, COUNT, VPT_FB_F64><<<grid, block, 0, stream>>>(K, S);
-    } else {
-        if (K.fb == VPT_FB_F32) render_kernel<1, COUNT, VPT_FB_F32><<<grid, block, 0, stream>>>(K, S);
-        else render_kernel<1, COUNT, VPT_FB_F64><<<grid, block, 0, stream>>>(K, S);
+    if (env_int("VPT_SIMPLE_KERNEL", 0)) {  /* A/B: one lane = one pixel, samples in sequence */
+        dim3 grid((unsigned)((K.w + 15) / 16), (unsigned)((K.shard_rows + 15) / 16));
+        render_kernel_simple<EST, COUNT, FB><<<grid, dim3(256), 0, stream>>>(K, S);
+        HIP_OK(hipGetLastError());
+        return VPT_OK;
     }
+    int blocks = 0;
+    int rc = persistent_grid(ctx, render_kernel<EST, COUNT, FB>, &blocks);
+    if (rc) return rc;
+    const int tiles = K.tiles_x * K.tiles_y;
+    const int need = (tiles + 3) / 4;  /* 4 waves per block, one tile per wave to start */
+    if (blocks > need) blocks = need;
+    if (blocks < 1) blocks = 1;
+    K.queue = ctx->d_queue;
+    HIP_OK(hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned), stream));
+    render_kernel<EST, COUNT, FB><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(K, S);
     HIP_OK(hipGetLastError());
     return VPT_OK;
+}
+
+template <bool COUNT>
+static int launch_render(vpt_context* ctx, KParams K, hipStream_t stream)
+{
+    if (K.shard_rows == 0) return VPT_OK;
+    K.tiles_x = (K.w + 7) / 8;
+    K.tiles_y = (K.shard_rows + 7) / 8;
+    K.cost_surf = env_int("VPT_COST_SURF", 1);
+    K.cost_med = env_int("VPT_COST_MED", 1);
+    if (K.est == VPT_FREE_FLIGHT) {
+        if (K.fb == VPT_FB_F32) return launch_one<0, COUNT, VPT_FB_F32>(ctx, K, stream);
+        return launch_one<0, COUNT, VPT_FB_F64>(ctx, K, stream);
+    }
+    if (K.fb == VPT_FB_F32) return launch_one<1, COUNT, VPT_FB_F32>(ctx, K, stream);
+    return launch_one<1, COUNT, VPT_FB_F64>(ctx, K, stream);
 }
 
 extern "C" {
@@ -235,8 +434,10 @@ int vpt_context_create(int device, vpt_context** out)
     c->has_scene = 0;
     c->d_scene = nullptr;
     c->d_counters = nullptr;
+    c->d_queue = nullptr;
     hipError_t e = hipMalloc((void**)&c->d_scene, sizeof(DevScene));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) c->d_queue = (unsigned*)(c->d_counters + 2);
     if (e != hipSuccess) {
         vpt_context_destroy(c);
         return vpt_fail(VPT_E_HIP, "vpt_context_create: hipMalloc: %s", hipGetErrorString(e));
@@ -314,6 +515,7 @@ int vpt_render(vpt_context* ctx, const vpt_params* p, void* h_out)
     if (rc) return rc;
     HIP_OK(hipSetDevice(ctx->device));
     size_t bytes = (size_t)K.shard_rows * (size_t)K.w * 3 * (K.fb == VPT_FB_F32 ? sizeof(float) : sizeof(double));
+    if (bytes == 0) return VPT_OK;
     void* d = nullptr;
     HIP_OK(hipMalloc(&d, bytes));
     K.out = d;
@@ -333,6 +535,11 @@ int vpt_count_work(vpt_context* ctx, const vpt_params* p, uint64_t* tests, uint6
     if (rc) return rc;
     HIP_OK(hipSetDevice(ctx->device));
     size_t bytes = (size_t)K.shard_rows * (size_t)K.w * 3 * (K.fb == VPT_FB_F32 ? sizeof(float) : sizeof(double));
+    if (bytes == 0) {
+        if (tests) *tests = 0;
+        if (iterations) *iterations = 0;
+        return VPT_OK;
+    }
     void* d = nullptr;
     HIP_OK(hipMalloc(&d, bytes));
     K.out = d;

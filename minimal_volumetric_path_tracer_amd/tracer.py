@@ -128,7 +128,8 @@ class Tracer:
         p = cfg.params()
         rows = int(lib().vpt_shard_rows(byref(p)))
         out = np.zeros((rows, cfg.width, 3), dtype=np.float64 if cfg.fp64 else np.float32)
-        check(lib().vpt_render(self._ctx, byref(p), out.ctypes.data))
+        if rows:
+            check(lib().vpt_render(self._ctx, byref(p), out.ctypes.data))
         return out
 
     def render_device(self, cfg: RenderConfig, out_ptr: int, stream: int = 0) -> None:

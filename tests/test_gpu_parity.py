@@ -84,10 +84,16 @@ def test_trace_batch_vs_reference(gpu_tracer, samples, scene, est):
     ref = samples[k + "L"]
     # same random draws consumed (the event sequence is the reference's) for nearly every sample
     assert (s == samples[k + "state2"]).mean() >= 0.97
-    # green / blue: reference value up to the libm ulp differences of this build's math
-    gb, rgb = L[:, 1:], ref[:, 1:]
-    ok = bitwise_equal(gb, rgb) | (np.abs(gb - rgb) <= 1e-9 * np.maximum(np.abs(rgb), 1e-12))
-    assert ok.all(1).mean() >= 0.97
+    close = bitwise_equal(L, ref) | (np.abs(L - ref) <= 1e-9 * np.maximum(np.abs(ref), 1e-12))
+    # every channel: the reference value up to this build's libm ulps, except samples whose
+    # point-light rounding coin flip was re-rolled by an ulp-moved vertex
+    assert close.all(1).mean() >= 0.88
+    # channels no point light emits into are untouched by H5: they agree for nearly all samples
+    sc = samples[f"{scene}__scene"].view(vpt.SPHERE_DTYPE)
+    pl = sc[(sc["r"] == 0) & (sc["radiance"].max(1) > 0)]
+    for ch in range(3):
+        if len(pl) == 0 or (pl["radiance"][:, ch] == 0).all():
+            assert close[:, ch].mean() >= 0.97
 
 
 # ---------------------------------------------------------------- renders
