@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import minimal_volumetric_path_tracer_amd as vpt  # noqa: E402
+from minimal_volumetric_path_tracer_amd.distributed import gather_image  # noqa: E402
 
 METRIC = "Msamples/s (pixels×spp/s) at 1024²; per-channel RMSE vs CPU PPM"
 FLOP_PER_TEST = 20          # Sphere::intersect, include/Sphere.h:27-37
@@ -74,6 +75,26 @@ def cpu_baseline(threads: int) -> dict:
             "sample": f"oracle restatement (per-sample streams), 1024x256x8 spp free-flight, {threads} threads"}
 
 
+def pmc_traffic(config: str, world: int):
+    """HBM bytes per launch of render_kernel from the committed rocprofv3 PMC passes of this same
+    command (profiles/<round>/pmc_render_kernel.json, scripts/pmc.sh): (2 * FETCH_SIZE +
+    WRITE_SIZE) * 1 KiB -- gfx950 FETCH_SIZE reports half of a streamed read (MI355X_MICROARCH.md,
+    HBM).  Counters cannot be read live without the profiler; None when no profile matches."""
+    if config != "ff" or world != 1:
+        return None
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_render_kernel.json"))):
+        try:
+            d = json.load(open(f))
+            c = d["counters"]
+            best = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+        except (OSError, KeyError, ValueError):
+            continue
+    return best
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,7 +128,6 @@ def main() -> None:
     tracer = vpt.Tracer(dev.index)
     rows = cfg.shard_rows()
     out = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)
-    gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
     image = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if rank == 0 else None
     stream = torch.cuda.current_stream(dev)
 
@@ -125,11 +145,9 @@ def main() -> None:
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            dist.gather(out, gathered, dst=0)
+            full = gather_image(out, cfg, band_rows=band)  # RCCL gather of the strips to rank 0
             if rank == 0:
-                g = torch.stack(gathered)  # (world, bands_per_rank*band, W, 3)
-                nb = rows // band
-                image.copy_(g.view(world, nb, band, W, 3).permute(1, 0, 2, 3, 4).reshape(H, W, 3))
+                image.copy_(full)
         elif rank == 0:
             image.copy_(out)
 
@@ -186,7 +204,7 @@ def main() -> None:
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
-                "traffic": None,
+                "traffic": pmc_traffic(args.config, world),
                 "kernel": "render_kernel<FF>",
                 "kernel_ms": round(kern_ms, 3),
                 "algorithmic": f"{FLOP_PER_TEST} FP64 flop x {T:.2f} ray-sphere tests per sample (SURVEY 8d) x "

@@ -13,7 +13,8 @@ from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint6
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libvpt.so")
+# VPT_LIB: path of an alternative build of the same ABI (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("VPT_LIB") or os.path.join(PKG_DIR, "libvpt.so")
 CLI_PATH = os.path.join(PKG_DIR, "vpt")
 
 VPT_OK = 0

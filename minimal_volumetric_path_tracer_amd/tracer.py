@@ -127,10 +127,9 @@ class Tracer:
         cfg = cfg or RenderConfig(**kw)
         p = cfg.params()
         rows = int(lib().vpt_shard_rows(byref(p)))
-        out = np.zeros((rows, cfg.width, 3), dtype=np.float64 if cfg.fp64 else np.float32)
-        if rows:
-            check(lib().vpt_render(self._ctx, byref(p), out.ctypes.data))
-        return out
+        out = np.zeros((max(rows, 1), cfg.width, 3), dtype=np.float64 if cfg.fp64 else np.float32)
+        check(lib().vpt_render(self._ctx, byref(p), out.ctypes.data))  # validates even an empty shard
+        return out[:rows]
 
     def render_device(self, cfg: RenderConfig, out_ptr: int, stream: int = 0) -> None:
         """Enqueues a render into a device buffer (e.g. torch tensor .data_ptr()) on `stream`."""

@@ -1,0 +1,28 @@
+#!/usr/bin/env bash
+# PMC counter passes over one bench step (each pass its own rocprofv3 run, kernel-trace only).
+# usage: bash scripts/pmc.sh <tag> [bench args...]
+set -u
+TAG=${1:-r01}
+shift || true
+ARGS=${*:---steps 1 --warmup 0 --no-cpu}
+OUT=gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+PASSES=(
+  "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM"
+  "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_CVT"
+  "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_INSTS_VSKIPPED GRBM_GUI_ACTIVE"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+)
+i=0
+for p in "${PASSES[@]}"; do
+    i=$((i + 1))
+    echo "== pass $i: $p"
+    timeout -k 10 600 rocprofv3 --pmc $p --kernel-trace -d "$OUT/p$i" -o run --output-format csv -- \
+        python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
+    rc=$?
+    echo "rc=$rc"
+    case $rc in 0) ;; *) tail -5 "$OUT/p$i.log"; echo "STOP"; exit $rc ;; esac
+done
+echo "== done"
