@@ -94,7 +94,11 @@ typedef struct vpt_params {
      * and writes them compactly, in increasing file-row order.  Whole image: band_rows = height,
      * band_stride = 1, band_offset = 0 (vpt_default_params). */
     int32_t band_rows, band_stride, band_offset;
-    int32_t reserved_;
+    /* Samples per partial sum (build extension; 0 = auto = ceil(spp/16)).  A pixel's samples are
+     * summed sequentially inside a chunk exactly as the reference sums a pixel (src/rt.cpp:794),
+     * and the chunk sums are then added in chunk order; chunk_spp == 1 or >= spp is the
+     * reference's own sequential order.  Chunks are the GPU's unit of work. */
+    int32_t chunk_spp;
 } vpt_params;
 
 /* Fills the reference defaults: 1024x768, spp 16, free-flight, sigma 0.001/0.009, camera and

@@ -62,7 +62,7 @@ class vpt_params(ctypes.Structure):
         ("band_rows", c_int32),
         ("band_stride", c_int32),
         ("band_offset", c_int32),
-        ("reserved_", c_int32),
+        ("chunk_spp", c_int32),
     ]
 
 

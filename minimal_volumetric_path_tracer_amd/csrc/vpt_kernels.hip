@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include "vpt_device.h"
+#include "vpt_pool.h"
 #include "vpt_internal.h"
 
 using namespace vpt;
@@ -32,6 +33,7 @@ struct KParams {
     unsigned* queue;               /* pixel work queue head (zeroed before each launch) */
     int32_t tiles_x, tiles_y;      /* 8x8 pixel tiles covering the shard */
     int32_t cost_surf, cost_med;   /* event scheduler weights */
+    int32_t chunk;                 /* samples per partial sum (pool kernel) */
 };
 
 #define HIP_OK(expr)                                                                         \
@@ -296,6 +298,8 @@ struct vpt_context {
     int has_scene;
     unsigned long long* d_counters;
     unsigned* d_queue;
+    double* d_partials;      /* chunk sums of the pool kernel, grown on demand */
+    size_t partials_bytes;
 };
 
 static int check_medium(const vpt_medium* m)
@@ -357,6 +361,8 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
     K.cy[1] = cry * inv * p->fov_scale;
     K.cy[2] = crz * inv * p->fov_scale;
     K.out = d_out;
+    if (p->chunk_spp < 0) return vpt_fail(VPT_E_INVALID, "chunk_spp must be >= 0");
+    K.chunk = p->chunk_spp > 0 ? (p->chunk_spp < p->spp ? p->chunk_spp : p->spp) : (p->spp + 15) / 16;
     return VPT_OK;
 }
 
@@ -388,7 +394,53 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         return VPT_OK;
     }
     int blocks = 0;
-    int rc = persistent_grid(ctx, render_kernel<EST, COUNT, FB>, &blocks);
+    int rc;
+    if (!env_int("VPT_WAVE_KERNEL", 0)) {  /* default: workgroup task pool (vpt_pool.h) */
+        PoolParams Q;
+        Q.w = K.w;
+        Q.h = K.h;
+        Q.spp = K.spp;
+        Q.rows = K.shard_rows;
+        Q.band_rows = K.band_rows;
+        Q.band_stride = K.band_stride;
+        Q.band_offset = K.band_offset;
+        Q.tiles_x = K.tiles_x;
+        Q.chunk = K.chunk;
+        Q.nch = (K.spp + K.chunk - 1) / K.chunk;
+        const uint64_t units = (uint64_t)K.tiles_x * (uint64_t)K.tiles_y * 64u * (uint64_t)Q.nch;
+        if (units >= 0xFFFFFFFFull) return vpt_fail(VPT_E_INVALID, "too many work units (%llu)", (unsigned long long)units);
+        Q.nunits = (unsigned)units;
+        Q.seed = K.seed;
+        for (int i = 0; i < 3; ++i) {
+            Q.o[i] = K.o[i];
+            Q.d[i] = K.d[i];
+            Q.cx[i] = K.cx[i];
+            Q.cy[i] = K.cy[i];
+        }
+        const size_t pbytes = (size_t)K.shard_rows * (size_t)K.w * (size_t)Q.nch * 3 * sizeof(double);
+        if (pbytes > ctx->partials_bytes) {
+            if (ctx->d_partials) HIP_OK(hipFree(ctx->d_partials));
+            ctx->d_partials = nullptr;
+            ctx->partials_bytes = 0;
+            HIP_OK(hipMalloc((void**)&ctx->d_partials, pbytes));
+            ctx->partials_bytes = pbytes;
+        }
+        Q.partials = ctx->d_partials;
+        Q.queue = ctx->d_queue;
+        const Medium m{K.sigma_a, K.sigma_s, K.g, K.max_depth};
+        rc = persistent_grid(ctx, pool_kernel<EST, COUNT>, &blocks);
+        if (rc) return rc;
+        const uint64_t need = (units + POOL - 1) / POOL;
+        if ((uint64_t)blocks > need) blocks = (int)need;
+        HIP_OK(hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned), stream));
+        pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(Q, m, S, K.counters);
+        HIP_OK(hipGetLastError());
+        const size_t npix = (size_t)K.shard_rows * (size_t)K.w;
+        reduce_kernel<FB><<<dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream>>>(Q, K.out);
+        HIP_OK(hipGetLastError());
+        return VPT_OK;
+    }
+    rc = persistent_grid(ctx, render_kernel<EST, COUNT, FB>, &blocks);
     if (rc) return rc;
     const int tiles = K.tiles_x * K.tiles_y;
     const int need = (tiles + 3) / 4;  /* 4 waves per block, one tile per wave to start */
@@ -435,6 +487,8 @@ int vpt_context_create(int device, vpt_context** out)
     c->d_scene = nullptr;
     c->d_counters = nullptr;
     c->d_queue = nullptr;
+    c->d_partials = nullptr;
+    c->partials_bytes = 0;
     hipError_t e = hipMalloc((void**)&c->d_scene, sizeof(DevScene));
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long));
     if (e == hipSuccess) c->d_queue = (unsigned*)(c->d_counters + 2);
@@ -454,6 +508,7 @@ void vpt_context_destroy(vpt_context* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->d_scene) (void)hipFree(ctx->d_scene);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_partials) (void)hipFree(ctx->d_partials);
     (void)hipSetDevice(prev);
     delete ctx;
 }

@@ -1,0 +1,353 @@
+/*
+ * vpt_pool.h -- workgroup task pool in LDS: cross-wave compaction of pending path events.
+ *
+ * A task is one (pixel, chunk of samples) work unit in flight: its path state (ray, throughput,
+ * radiance, chunk sum, erand48 state, pending event) lives in LDS, not in a lane.  A path loop
+ * iteration of the reference (include/vptShadeMethods.h:1278-1336 / :1345-1481) is split into three
+ * stages:
+ *     A  roulette + intersection + light pick + distance sample   (decide(), vpt_device.h)
+ *     S  surface event: pLight + MISv2 + bdsf                      (surface_event())
+ *     M  medium event: single scattering + phase sample            (medium_event())
+ * Each stage keeps a ring of task slots.  A wave takes the lock, returns its finished tasks to the
+ * rings of their next stage, takes up to 64 tasks of the fullest stage, releases the lock, loads
+ * those states, runs that ONE stage with (nearly) every lane busy, and stores the states back.  The
+ * pool is larger than the workgroup (POOL > 256), so there is nearly always a full batch of some
+ * stage: no wave runs a block with half its lanes idle, and no wave waits for its longest path.
+ *
+ * Determinism: a task runs its unit's samples strictly in order and adds each sample to the
+ * chunk sum as the reference adds to its pixel (acc = L + acc, src/rt.cpp:794); chunk sums are
+ * written to a partial buffer and combined in chunk order by reduce_kernel.  Which wave or lane
+ * runs a stage changes nothing in the arithmetic, so images are bit-identical to the oracle
+ * (oracle/vpt_oracle.c orc_render_chunked) for any schedule, GPU count or pool size.
+ */
+#ifndef VPT_POOL_H
+#define VPT_POOL_H
+
+#include "vpt_device.h"
+
+namespace vpt {
+
+constexpr int POOL = 448;        /* task slots per workgroup (256 lanes) -- ~76 KB of LDS, 2 WGs/CU */
+constexpr int NF = 18;           /* doubles per task */
+constexpr unsigned NO_UNIT = 0xFFFFFFFFu;
+enum { ST_A = 0, ST_S = 1, ST_M = 2, ST_DONE = 3 };
+enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_BX, F_BY, F_BZ, F_LX, F_LY, F_LZ, F_AX, F_AY, F_AZ, F_T, F_DIST,
+       F_PDF };
+
+struct TaskPool {
+    double f[NF][POOL];     /* SoA: one array per field */
+    uint64_t X[POOL];       /* erand48 state */
+    uint32_t unit[POOL];    /* work unit, NO_UNIT when the task needs a new one */
+    uint32_t samp[POOL];    /* next sample to start | in_path << 31 */
+    uint32_t evw[POOL];     /* depth | id << 16 | src << 24 */
+    uint16_t ring[3][POOL]; /* slots waiting for stage A / S / M */
+    int head[3], tail[3];   /* monotonic ring counters */
+    int done;               /* slots retired (work queue exhausted) */
+    int lock;
+};
+
+struct PoolParams {
+    int w, h, spp, rows;
+    int band_rows, band_stride, band_offset;
+    int tiles_x, nch, chunk;
+    unsigned nunits;
+    uint64_t seed;
+    double o[3], d[3], cx[3], cy[3];
+    double* partials;       /* rows * w * nch * 3 */
+    unsigned* queue;
+};
+
+/* work unit -> pixel (8x8 tile order: a batch of 64 consecutive units is one tile, one chunk) */
+struct Unit {
+    int x, lr, y, c;
+    uint64_t idx;
+    bool valid;
+};
+
+__device__ __forceinline__ Unit decode_unit(const PoolParams& P, unsigned u)
+{
+    Unit r;
+    const unsigned per_tile = 64u * (unsigned)P.nch;
+    const unsigned tile = u / per_tile, rem = u - tile * per_tile;
+    r.c = (int)(rem >> 6);
+    const unsigned p = rem & 63u;
+    r.x = (int)(tile % (unsigned)P.tiles_x) * 8 + (int)(p & 7u);
+    r.lr = (int)(tile / (unsigned)P.tiles_x) * 8 + (int)(p >> 3);
+    r.valid = r.x < P.w && r.lr < P.rows;
+    const int k = r.lr / P.band_rows, rr = r.lr - k * P.band_rows;
+    const int fr = (P.band_offset + k * P.band_stride) * P.band_rows + rr;  /* file row */
+    r.y = P.h - 1 - fr;                                                       /* camera row */
+    r.idx = (uint64_t)fr * (uint64_t)P.w + (uint64_t)r.x;                     /* src/rt.cpp:773 */
+    return r;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ dv3 pool_camera_dir(const PoolParams& P, Sampler<COUNT>& smp, int x, int y)
+{
+    const dv3 cd = mk(P.d[0], P.d[1], P.d[2]);
+    const dv3 cx = mk(P.cx[0], P.cx[1], P.cx[2]), cy = mk(P.cy[0], P.cy[1], P.cy[2]);
+    double jx = smp.next();  /* src/rt.cpp:787, x draw first */
+    double jy = smp.next();
+    dv3 dir = add(add(scl(cx, (((double)x + jx - 0.5) / P.w - .5)), scl(cy, (((double)y + jy - 0.5) / P.h - .5))), cd);
+    return nrm(dir);
+}
+
+/* ---- task state <-> registers ---- */
+struct Task {
+    Path p;
+    Event e;
+    dv3 acc;
+    uint64_t X;
+    unsigned unit;
+    unsigned i;
+    bool in_path;
+};
+
+__device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bool full)
+{
+    t.p.o = mk(sh.f[F_OX][s], sh.f[F_OY][s], sh.f[F_OZ][s]);
+    t.p.d = mk(sh.f[F_DX][s], sh.f[F_DY][s], sh.f[F_DZ][s]);
+    t.p.beta = mk(sh.f[F_BX][s], sh.f[F_BY][s], sh.f[F_BZ][s]);
+    t.p.L = mk(sh.f[F_LX][s], sh.f[F_LY][s], sh.f[F_LZ][s]);
+    t.e.t = sh.f[F_T][s];
+    t.e.dist = sh.f[F_DIST][s];
+    t.e.pdf = sh.f[F_PDF][s];
+    const uint32_t ev = sh.evw[s];
+    t.p.depth = (int)(ev & 0xFFFFu);
+    t.e.id = (int)((ev >> 16) & 0xFFu);
+    t.e.src = (int)(ev >> 24);
+    t.X = sh.X[s];
+    if (full) {
+        t.acc = mk(sh.f[F_AX][s], sh.f[F_AY][s], sh.f[F_AZ][s]);
+        t.unit = sh.unit[s];
+        const uint32_t sm = sh.samp[s];
+        t.i = sm & 0x7FFFFFFFu;
+        t.in_path = (sm >> 31) != 0;
+    }
+}
+
+__device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, bool full)
+{
+    sh.f[F_OX][s] = t.p.o.x; sh.f[F_OY][s] = t.p.o.y; sh.f[F_OZ][s] = t.p.o.z;
+    sh.f[F_DX][s] = t.p.d.x; sh.f[F_DY][s] = t.p.d.y; sh.f[F_DZ][s] = t.p.d.z;
+    sh.f[F_BX][s] = t.p.beta.x; sh.f[F_BY][s] = t.p.beta.y; sh.f[F_BZ][s] = t.p.beta.z;
+    sh.f[F_LX][s] = t.p.L.x; sh.f[F_LY][s] = t.p.L.y; sh.f[F_LZ][s] = t.p.L.z;
+    sh.X[s] = t.X;
+    sh.evw[s] = (uint32_t)(t.p.depth & 0xFFFF) | ((uint32_t)t.e.id << 16) | ((uint32_t)t.e.src << 24);
+    if (full) {
+        sh.f[F_T][s] = t.e.t;
+        sh.f[F_DIST][s] = t.e.dist;
+        sh.f[F_PDF][s] = t.e.pdf;
+        sh.f[F_AX][s] = t.acc.x; sh.f[F_AY][s] = t.acc.y; sh.f[F_AZ][s] = t.acc.z;
+        sh.unit[s] = t.unit;
+        sh.samp[s] = t.i | (t.in_path ? 0x80000000u : 0u);
+    }
+}
+
+__device__ __forceinline__ void store_partial(const PoolParams& P, const Unit& u, dv3 acc)
+{
+    const size_t o = (((size_t)u.lr * (size_t)P.w + (size_t)u.x) * (size_t)P.nch + (size_t)u.c) * 3;
+    P.partials[o] = acc.x;
+    P.partials[o + 1] = acc.y;
+    P.partials[o + 2] = acc.z;
+}
+
+/* Stage A for the lanes with `active`: make every task either pending S/M or retired.  Returns
+ * the task's next stage.  Converged loop around a divergent one: lanes that need a work unit
+ * take them together (one queue atomic per round), lanes that have one advance their path. */
+template <int EST, bool COUNT>
+__device__ __forceinline__ int stage_a(const PoolParams& P, const DevScene* __restrict__ S, const Medium& m,
+                                       Sampler<COUNT>& smp, Task& t, bool active, int lane, uint64_t below)
+{
+    int result = active ? -1 : ST_DONE;
+    const dv3 o0 = mk(P.o[0], P.o[1], P.o[2]);
+    while (true) {
+        const bool need = result < 0 && t.unit == NO_UNIT;
+        const uint64_t needm = __ballot(need);
+        if (needm) {
+            const int leader = __ffsll((unsigned long long)needm) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(P.queue, (unsigned)__popcll(needm));
+            base = __shfl(base, leader);
+            if (need) {
+                const unsigned u = base + (unsigned)__popcll(needm & below);
+                if (u >= P.nunits) {
+                    result = ST_DONE;
+                } else if (decode_unit(P, u).valid) {
+                    t.unit = u;
+                    t.i = (unsigned)(decode_unit(P, u).c * P.chunk);
+                    t.in_path = false;
+                    t.acc = mk(0, 0, 0);
+                }
+            }
+        }
+        if (result < 0 && t.unit != NO_UNIT) {
+            const Unit u = decode_unit(P, t.unit);
+            const unsigned c1 = (unsigned)min((u.c + 1) * P.chunk, P.spp);
+            smp.X = t.X;
+            while (true) {
+                if (!t.in_path) {
+                    if (t.i == c1) {
+                        store_partial(P, u, t.acc);
+                        t.unit = NO_UNIT;
+                        break;
+                    }
+                    smp.X = vpt_stream_start(P.seed, u.idx, (uint64_t)t.i);
+                    ++t.i;
+                    t.p.o = o0;
+                    t.p.d = pool_camera_dir(P, smp, u.x, u.y);
+                    t.p.beta = mk(1, 1, 1);
+                    t.p.L = mk(0, 0, 0);
+                    t.p.depth = 0;
+                    t.in_path = true;
+                }
+                if (!continue_path(smp, t.p, m)) {
+                    t.acc = add(t.p.L, t.acc);  /* src/rt.cpp:794 */
+                    t.in_path = false;
+                    continue;
+                }
+                const int ev = decide<EST>(S, smp, t.p, t.e, m);
+                if (ev == EV_END) {
+                    t.acc = add(t.p.L, t.acc);
+                    t.in_path = false;
+                    continue;
+                }
+                result = ev == EV_SURF ? ST_S : ST_M;
+                break;
+            }
+            t.X = smp.X;
+        }
+        if (__ballot(result < 0) == 0) break;
+    }
+    return result;
+}
+
+template <int EST, bool COUNT>
+__global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, const DevScene* __restrict__ S,
+                                                   unsigned long long* counters)
+{
+    __shared__ TaskPool sh;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int j = tid; j < POOL; j += 256) {
+        sh.unit[j] = NO_UNIT;
+        sh.samp[j] = 0;
+        sh.evw[j] = 0;
+        sh.ring[ST_A][j] = (uint16_t)j;
+    }
+    if (tid == 0) {
+        sh.head[0] = sh.head[1] = sh.head[2] = 0;
+        sh.tail[ST_A] = POOL;
+        sh.tail[ST_S] = sh.tail[ST_M] = 0;
+        sh.done = 0;
+        sh.lock = 0;
+    }
+    __syncthreads();
+
+    Sampler<COUNT> smp;
+    smp.X = 0;
+    smp.g = m.g;
+    smp.cnt.tests = 0;
+    smp.cnt.iterations = 0;
+    int n = 0, slot = 0, next = ST_A;
+    while (true) {
+        /* ---- critical section: return finished tasks, take a batch of the fullest stage ---- */
+        if (lane == 0) {
+            int expected = 0;
+            while (!__hip_atomic_compare_exchange_strong(&sh.lock, &expected, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                expected = 0;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (n > 0) {
+#pragma unroll
+            for (int T = 0; T < 3; ++T) {
+                const bool mine = lane < n && next == T;
+                const uint64_t msk = __ballot(mine);
+                if (msk) {
+                    const int base = sh.tail[T];
+                    if (mine) sh.ring[T][(base + __popcll(msk & below)) % POOL] = (uint16_t)slot;
+                    if (lane == 0) sh.tail[T] = base + __popcll(msk);
+                }
+            }
+            const uint64_t md = __ballot(lane < n && next == ST_DONE);
+            if (lane == 0 && md) sh.done += __popcll(md);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const int done = __builtin_amdgcn_readfirstlane(sh.done);
+        int cnt[3];
+#pragma unroll
+        for (int T = 0; T < 3; ++T) cnt[T] = __builtin_amdgcn_readfirstlane(sh.tail[T] - sh.head[T]);
+        int st = cnt[ST_M] >= cnt[ST_S] ? ST_M : ST_S;
+        if (cnt[ST_A] > cnt[st]) st = ST_A;
+        const int take = min(64, cnt[st]);
+        if (take > 0) {
+            const int h0 = sh.head[st];
+            if (lane < take) slot = sh.ring[st][(h0 + lane) % POOL];
+            if (lane == 0) sh.head[st] = h0 + take;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&sh.lock, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        n = take;
+        if (done == POOL) break;
+        if (take == 0) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+
+        /* ---- run one stage on the batch ---- */
+        const bool active = lane < n;
+        Task t;
+        if (st == ST_A) {
+            if (active) load_task(sh, slot, t, true);
+            else {
+                t.unit = NO_UNIT;
+                t.in_path = false;
+            }
+            next = stage_a<EST>(P, S, m, smp, t, active, lane, below);
+            if (active) store_task(sh, slot, t, true);
+        } else if (active) {
+            load_task(sh, slot, t, false);
+            smp.X = t.X;
+            if (st == ST_S) surface_event<EST>(S, smp, t.p, t.e, m);
+            else medium_event<EST>(S, smp, t.p, t.e, m);
+            t.X = smp.X;
+            store_task(sh, slot, t, false);
+            next = ST_A;
+        }
+    }
+    if (COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)smp.cnt.tests);
+        atomicAdd(&counters[1], (unsigned long long)smp.cnt.iterations);
+    }
+}
+
+/* chunk sums -> pixel average, in chunk order (matches orc_render_chunked) */
+template <int FB>
+__global__ __launch_bounds__(256) void reduce_kernel(PoolParams P, void* out)
+{
+    const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t npix = (size_t)P.rows * (size_t)P.w;
+    if (p >= npix) return;
+    const double* q = P.partials + p * (size_t)P.nch * 3;
+    dv3 tot = mk(0, 0, 0);
+    for (int c = 0; c < P.nch; ++c) tot = add(mk(q[3 * c], q[3 * c + 1], q[3 * c + 2]), tot);
+    tot = scl(tot, (1 / (double)P.spp));  /* src/rt.cpp:800 */
+    if (FB == VPT_FB_F32) {
+        float* o = (float*)out;
+        o[3 * p] = (float)tot.x;
+        o[3 * p + 1] = (float)tot.y;
+        o[3 * p + 2] = (float)tot.z;
+    } else {
+        double* o = (double*)out;
+        o[3 * p] = tot.x;
+        o[3 * p + 1] = tot.y;
+        o[3 * p + 2] = tot.z;
+    }
+}
+
+}  // namespace vpt
+
+#endif

@@ -73,6 +73,7 @@ class RenderConfig:
     band_rows: int = 0          # 0 = whole image
     band_stride: int = 1
     band_offset: int = 0
+    chunk_spp: int = 0          # 0 = auto (ceil(spp/16)); 1 or >= spp = the reference's sequential sum
 
     def params(self) -> _lib.vpt_params:
         p = _lib.vpt_params()
@@ -85,6 +86,7 @@ class RenderConfig:
         p.seed = self.seed
         p.band_rows = self.band_rows if self.band_rows > 0 else self.height
         p.band_stride, p.band_offset = self.band_stride, self.band_offset
+        p.chunk_spp = self.chunk_spp
         return p
 
     def shard_rows(self) -> int:

@@ -66,6 +66,11 @@ def _bind(L: ctypes.CDLL, prefix: str) -> ctypes.CDLL:
     return L
 
 
+def default_chunk(spp: int) -> int:
+    """samples per chunk the GPU uses when vpt_params.chunk_spp == 0 (csrc/vpt_kernels.hip)"""
+    return max(1, (spp + 15) // 16)
+
+
 class Oracle:
     """liboracle.so (portable=False) or liboracle_vm.so (portable=True)."""
 
@@ -80,6 +85,8 @@ class Oracle:
         L.orc_trace.argtypes = [_P, _U, POINTER(Medium), _P, POINTER(Counters)]
         L.orc_render.restype = None
         L.orc_render.argtypes = [_I, _I, _I, POINTER(Medium), _U, _I, _I, _P, _I, POINTER(Counters)]
+        L.orc_render_chunked.restype = None
+        L.orc_render_chunked.argtypes = [_I, _I, _I, _I, POINTER(Medium), _U, _I, _I, _P, _I, POINTER(Counters)]
         L.orc_write_ppm.restype, L.orc_write_ppm.argtypes = _I, [ctypes.c_char_p, _P, _I, _I]
         L.orc_stream_state_c.restype, L.orc_stream_state_c.argtypes = _U, [_U, _U, _U]
         L.orc_is_portable_math.restype = _I
@@ -110,12 +117,16 @@ class Oracle:
         return (out, st, tot) if counters else (out, st)
 
     def render(self, w, h, spp, estimator=0, sigma_a=0.001, sigma_s=0.009, hg_g=0.0, max_depth=0, seed=0x5EED0001,
-               y0=0, y1=None, threads=0, counters=False):
-        """main()'s pixel loop over camera rows [y0, y1); returns (h, w, 3) float64 in file order."""
+               y0=0, y1=None, threads=0, counters=False, chunk=None):
+        """main()'s pixel loop over camera rows [y0, y1); returns (h, w, 3) float64 in file order.
+        chunk: samples per partial sum (None = the GPU's default, ceil(spp/16); spp = reference order)."""
         m = Medium(sigma_a, sigma_s, hg_g, max_depth, estimator)
         out = np.zeros((h, w, 3))
         c = Counters()
-        self.L.orc_render(w, h, spp, byref(m), seed, y0, h if y1 is None else y1, out.ctypes.data, threads, byref(c))
+        if chunk is None:
+            chunk = default_chunk(spp)
+        self.L.orc_render_chunked(w, h, spp, chunk, byref(m), seed, y0, h if y1 is None else y1, out.ctypes.data,
+                                  threads, byref(c))
         return (out, c) if counters else out
 
     def math(self, fn: int, x: np.ndarray, y=None) -> np.ndarray:
