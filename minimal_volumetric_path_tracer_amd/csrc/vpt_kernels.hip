@@ -289,6 +289,8 @@ __global__ void math_probe_kernel(int fn, const double* x, const double* y, doub
 
 bool is_finite(double v) { return v == v && v - v == 0.0; }
 
+unsigned long long* g_pool_stats = nullptr;  /* debug statistics buffer (VPT_POOL_STATS=1) */
+
 }  // namespace
 
 struct vpt_context {
@@ -433,7 +435,13 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         const uint64_t need = (units + POOL - 1) / POOL;
         if ((uint64_t)blocks > need) blocks = (int)need;
         HIP_OK(hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned), stream));
-        pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(Q, m, S, K.counters);
+        unsigned long long* stats = nullptr;
+        if (env_int("VPT_POOL_STATS", 0)) {  /* debug: scheduler statistics, vpt_debug_pool_stats */
+            if (!g_pool_stats) HIP_OK(hipMalloc((void**)&g_pool_stats, 8 * sizeof(unsigned long long)));
+            HIP_OK(hipMemsetAsync(g_pool_stats, 0, 8 * sizeof(unsigned long long), stream));
+            stats = g_pool_stats;
+        }
+        pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(Q, m, S, K.counters, stats);
         HIP_OK(hipGetLastError());
         const size_t npix = (size_t)K.shard_rows * (size_t)K.w;
         reduce_kernel<FB><<<dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream>>>(Q, K.out);
@@ -677,3 +685,13 @@ int vpt_math_probe(vpt_context* ctx, int fn, const double* x, const double* y, d
 }
 
 }  // extern "C"
+
+/* Debug (not part of include/vpt.h): scheduler statistics of the last pool launch made with
+ * VPT_POOL_STATS=1 -- [batches A, S, M, lanes A, S, M, idle polls, lock retries]. */
+extern "C" int vpt_debug_pool_stats(unsigned long long* out)
+{
+    if (!g_pool_stats || !out) return VPT_E_INVALID;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(out, g_pool_stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return VPT_OK;
+}

@@ -43,8 +43,13 @@ struct TaskPool {
     uint16_t ring[3][POOL]; /* slots waiting for stage A / S / M */
     int head[3], tail[3];   /* monotonic ring counters */
     int done;               /* slots retired (work queue exhausted) */
-    int lock;
+    int ticket, serving;    /* FIFO ticket lock: a wave returning tasks is never starved */
 };
+
+__device__ __forceinline__ int lds_peek(const int* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 struct PoolParams {
     int w, h, spp, rows;
@@ -224,7 +229,7 @@ __device__ __forceinline__ int stage_a(const PoolParams& P, const DevScene* __re
 
 template <int EST, bool COUNT>
 __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, const DevScene* __restrict__ S,
-                                                   unsigned long long* counters)
+                                                   unsigned long long* counters, unsigned long long* stats)
 {
     __shared__ TaskPool sh;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -240,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
         sh.tail[ST_A] = POOL;
         sh.tail[ST_S] = sh.tail[ST_M] = 0;
         sh.done = 0;
-        sh.lock = 0;
+        sh.ticket = sh.serving = 0;
     }
     __syncthreads();
 
@@ -250,13 +255,31 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
     smp.cnt.tests = 0;
     smp.cnt.iterations = 0;
     int n = 0, slot = 0, next = ST_A;
+    unsigned long long st_batches[3] = {0, 0, 0}, st_lanes[3] = {0, 0, 0}, st_idle = 0, st_retry = 0;
     while (true) {
+        /* ---- an idle wave waits outside the lock until some ring has work (racy peek) ---- */
+        if (n == 0) {
+            bool fin = false;
+            while (true) {
+                const int pend = __builtin_amdgcn_readfirstlane(
+                    (lds_peek(&sh.tail[0]) - lds_peek(&sh.head[0])) + (lds_peek(&sh.tail[1]) - lds_peek(&sh.head[1])) +
+                    (lds_peek(&sh.tail[2]) - lds_peek(&sh.head[2])));
+                if (pend > 0) break;
+                if (__builtin_amdgcn_readfirstlane(lds_peek(&sh.done)) == POOL) {
+                    fin = true;
+                    break;
+                }
+                ++st_idle;
+                __builtin_amdgcn_s_sleep(4);
+            }
+            if (fin) break;
+        }
         /* ---- critical section: return finished tasks, take a batch of the fullest stage ---- */
+        int ticket = 0;
         if (lane == 0) {
-            int expected = 0;
-            while (!__hip_atomic_compare_exchange_strong(&sh.lock, &expected, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                expected = 0;
+            ticket = __hip_atomic_fetch_add(&sh.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            while (lds_peek(&sh.serving) != ticket) {
+                ++st_retry;
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -289,12 +312,17 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
             if (lane == 0) sh.head[st] = h0 + take;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&sh.lock, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_store(&sh.serving, ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         n = take;
         if (done == POOL) break;
         if (take == 0) {
+            ++st_idle;
             __builtin_amdgcn_s_sleep(2);
             continue;
+        }
+        if (stats) {
+            st_batches[st] += 1;
+            st_lanes[st] += (unsigned long long)take;
         }
 
         /* ---- run one stage on the batch ---- */
@@ -321,6 +349,14 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
     if (COUNT) {
         atomicAdd(&counters[0], (unsigned long long)smp.cnt.tests);
         atomicAdd(&counters[1], (unsigned long long)smp.cnt.iterations);
+    }
+    if (stats && lane == 0) {  /* debug: [batches A S M, lanes A S M, idle polls, lock retries] */
+        for (int T = 0; T < 3; ++T) {
+            atomicAdd(&stats[T], st_batches[T]);
+            atomicAdd(&stats[3 + T], st_lanes[T]);
+        }
+        atomicAdd(&stats[6], st_idle);
+        atomicAdd(&stats[7], st_retry);
     }
 }
 
