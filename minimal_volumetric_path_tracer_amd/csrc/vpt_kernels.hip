@@ -437,8 +437,8 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         HIP_OK(hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned), stream));
         unsigned long long* stats = nullptr;
         if (env_int("VPT_POOL_STATS", 0)) {  /* debug: scheduler statistics, vpt_debug_pool_stats */
-            if (!g_pool_stats) HIP_OK(hipMalloc((void**)&g_pool_stats, 8 * sizeof(unsigned long long)));
-            HIP_OK(hipMemsetAsync(g_pool_stats, 0, 8 * sizeof(unsigned long long), stream));
+            if (!g_pool_stats) HIP_OK(hipMalloc((void**)&g_pool_stats, NSTATS * sizeof(unsigned long long)));
+            HIP_OK(hipMemsetAsync(g_pool_stats, 0, NSTATS * sizeof(unsigned long long), stream));
             stats = g_pool_stats;
         }
         pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(Q, m, S, K.counters, stats);
@@ -687,11 +687,11 @@ int vpt_math_probe(vpt_context* ctx, int fn, const double* x, const double* y, d
 }  // extern "C"
 
 /* Debug (not part of include/vpt.h): scheduler statistics of the last pool launch made with
- * VPT_POOL_STATS=1 -- [batches A, S, M, lanes A, S, M, idle polls, lock retries]. */
+ * VPT_POOL_STATS=1 -- NSTATS counters, layout in vpt_pool.h. */
 extern "C" int vpt_debug_pool_stats(unsigned long long* out)
 {
     if (!g_pool_stats || !out) return VPT_E_INVALID;
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(out, g_pool_stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(out, g_pool_stats, NSTATS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return VPT_OK;
 }

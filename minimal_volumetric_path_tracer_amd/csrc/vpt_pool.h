@@ -30,6 +30,17 @@ namespace vpt {
 constexpr int POOL = 448;        /* task slots per workgroup (256 lanes) -- ~76 KB of LDS, 2 WGs/CU */
 constexpr int NF = 18;           /* doubles per task */
 constexpr unsigned NO_UNIT = 0xFFFFFFFFu;
+constexpr int URING = 256, UREFILL = 128;  /* per-workgroup work-unit ring: one global atomic per 128 units */
+/* debug statistics (VPT_POOL_STATS=1, vpt_debug_pool_stats): [0-2] batches A/S/M, [3-5] lanes
+ * A/S/M, [6] idle polls, [7] ticket waits, [8-10] cycles in stage A/S/M, [11] cycles scheduling,
+ * [12] stage-A preparation rounds, [14] decide() calls (lanes), [15] samples started */
+constexpr int NSTATS = 24;  /* [16] stage-A cycles in the preparation loop, [18] in decide,
+                               [19] task load/store */
+struct ADbg {
+    unsigned long long outer, lane_it, samples;
+    unsigned long long c_grab, c_decide, c_g, c_s, atomics;
+};
+__device__ __forceinline__ unsigned long long dbg_clock(bool dbg) { return dbg ? __builtin_amdgcn_s_memtime() : 0; }
 enum { ST_A = 0, ST_S = 1, ST_M = 2, ST_DONE = 3 };
 enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_BX, F_BY, F_BZ, F_LX, F_LY, F_LZ, F_AX, F_AY, F_AZ, F_T, F_DIST,
        F_PDF };
@@ -38,12 +49,16 @@ struct TaskPool {
     double f[NF][POOL];     /* SoA: one array per field */
     uint64_t X[POOL];       /* erand48 state */
     uint32_t unit[POOL];    /* work unit, NO_UNIT when the task needs a new one */
+    uint32_t pix[POOL];     /* x | camera row << 16 */
+    uint32_t c1[POOL];      /* one past the unit's last sample */
     uint32_t samp[POOL];    /* next sample to start | in_path << 31 */
     uint32_t evw[POOL];     /* depth | id << 16 | src << 24 */
     uint16_t ring[3][POOL]; /* slots waiting for stage A / S / M */
     int head[3], tail[3];   /* monotonic ring counters */
     int done;               /* slots retired (work queue exhausted) */
     int ticket, serving;    /* FIFO ticket lock: a wave returning tasks is never starved */
+    uint32_t uring[URING];  /* prefetched work units (refilled under the lock, taken by CAS on uhead) */
+    int uhead, utail, exhausted;
 };
 
 __device__ __forceinline__ int lds_peek(const int* p)
@@ -86,26 +101,29 @@ __device__ __forceinline__ Unit decode_unit(const PoolParams& P, unsigned u)
     return r;
 }
 
-template <bool COUNT>
-__device__ __forceinline__ dv3 pool_camera_dir(const PoolParams& P, Sampler<COUNT>& smp, int x, int y)
+/* camera ray through pixel (x, y) with jitter (jx, jy) -- src/rt.cpp:787-789 */
+__device__ __forceinline__ dv3 pool_camera_dir(const PoolParams& P, double jx, double jy, int x, int y)
 {
     const dv3 cd = mk(P.d[0], P.d[1], P.d[2]);
     const dv3 cx = mk(P.cx[0], P.cx[1], P.cx[2]), cy = mk(P.cy[0], P.cy[1], P.cy[2]);
-    double jx = smp.next();  /* src/rt.cpp:787, x draw first */
-    double jy = smp.next();
     dv3 dir = add(add(scl(cx, (((double)x + jx - 0.5) / P.w - .5)), scl(cy, (((double)y + jy - 0.5) / P.h - .5))), cd);
     return nrm(dir);
 }
 
-/* ---- task state <-> registers ---- */
+/* ---- task state <-> registers ----
+ * A task in ring A either has a path that has already survived this iteration's roulette draw
+ * (in_path; the draw is taken at the end of stage S/M, where it falls in the stream anyway) or
+ * needs its next sample.  `killed`: the S/M roulette ended the path, stage A adds L to the sum. */
 struct Task {
     Path p;
     Event e;
     dv3 acc;
     uint64_t X;
-    unsigned unit;
-    unsigned i;
-    bool in_path;
+    unsigned unit;   /* work unit, NO_UNIT when the task needs one */
+    unsigned pix;    /* x | camera row << 16 of the unit's pixel */
+    unsigned c1;     /* one past the unit's last sample */
+    unsigned i;      /* next sample to start */
+    bool in_path, killed;
 };
 
 __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bool full)
@@ -120,11 +138,14 @@ __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bo
     const uint32_t ev = sh.evw[s];
     t.p.depth = (int)(ev & 0xFFFFu);
     t.e.id = (int)((ev >> 16) & 0xFFu);
-    t.e.src = (int)(ev >> 24);
+    t.e.src = (int)((ev >> 24) & 0x7Fu);
+    t.killed = (ev >> 31) != 0;
     t.X = sh.X[s];
     if (full) {
         t.acc = mk(sh.f[F_AX][s], sh.f[F_AY][s], sh.f[F_AZ][s]);
         t.unit = sh.unit[s];
+        t.pix = sh.pix[s];
+        t.c1 = sh.c1[s];
         const uint32_t sm = sh.samp[s];
         t.i = sm & 0x7FFFFFFFu;
         t.in_path = (sm >> 31) != 0;
@@ -138,13 +159,16 @@ __device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, b
     sh.f[F_BX][s] = t.p.beta.x; sh.f[F_BY][s] = t.p.beta.y; sh.f[F_BZ][s] = t.p.beta.z;
     sh.f[F_LX][s] = t.p.L.x; sh.f[F_LY][s] = t.p.L.y; sh.f[F_LZ][s] = t.p.L.z;
     sh.X[s] = t.X;
-    sh.evw[s] = (uint32_t)(t.p.depth & 0xFFFF) | ((uint32_t)t.e.id << 16) | ((uint32_t)t.e.src << 24);
+    sh.evw[s] = (uint32_t)(t.p.depth & 0xFFFF) | ((uint32_t)t.e.id << 16) | ((uint32_t)t.e.src << 24) |
+                (t.killed ? 0x80000000u : 0u);
     if (full) {
         sh.f[F_T][s] = t.e.t;
         sh.f[F_DIST][s] = t.e.dist;
         sh.f[F_PDF][s] = t.e.pdf;
         sh.f[F_AX][s] = t.acc.x; sh.f[F_AY][s] = t.acc.y; sh.f[F_AZ][s] = t.acc.z;
         sh.unit[s] = t.unit;
+        sh.pix[s] = t.pix;
+        sh.c1[s] = t.c1;
         sh.samp[s] = t.i | (t.in_path ? 0x80000000u : 0u);
     }
 }
@@ -157,72 +181,126 @@ __device__ __forceinline__ void store_partial(const PoolParams& P, const Unit& u
     P.partials[o + 2] = acc.z;
 }
 
-/* Stage A for the lanes with `active`: make every task either pending S/M or retired.  Returns
- * the task's next stage.  Converged loop around a divergent one: lanes that need a work unit
- * take them together (one queue atomic per round), lanes that have one advance their path. */
+/* Stage A for the lanes with `active`: at most ONE decide() per task.  A converged preparation
+ * loop first gives every task a path that has survived its roulette draw.  Lanes that need a
+ * work unit take them together (one queue atomic per round); a finished unit writes its chunk
+ * sum; a task without a path starts samples until one survives its first roulette draw.  A camera
+ * sample killed by that draw has L = 0 and adds nothing to the sum (acc + 0 = acc exactly), so
+ * only its three draws (jitter x, jitter y, roulette; src/rt.cpp:787 + vptShadeMethods.h:1282)
+ * are taken and its camera ray is never built: the loop is ~100 integer/FP64 instructions a
+ * round.  Then every ready lane runs decide() once; a path that ends there goes back to ring A.
+ * Returns the task's next stage. */
 template <int EST, bool COUNT>
-__device__ __forceinline__ int stage_a(const PoolParams& P, const DevScene* __restrict__ S, const Medium& m,
-                                       Sampler<COUNT>& smp, Task& t, bool active, int lane, uint64_t below)
+__device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const DevScene* __restrict__ S, const Medium& m,
+                                       Sampler<COUNT>& smp, Task& t, bool active, int lane, uint64_t below,
+                                       bool dbg, ADbg& D)
 {
-    int result = active ? -1 : ST_DONE;
-    const dv3 o0 = mk(P.o[0], P.o[1], P.o[2]);
+    bool done = !active, parked = false;
+    if (active && t.killed) {  /* the S/M roulette ended the path */
+        t.acc = add(t.p.L, t.acc);  /* src/rt.cpp:794 */
+        t.in_path = false;
+        t.killed = false;
+    }
+    const unsigned long long c0 = dbg_clock(dbg);
     while (true) {
-        const bool need = result < 0 && t.unit == NO_UNIT;
+        if (dbg) ++D.outer;
+        const unsigned long long g0 = dbg_clock(dbg);
+        const bool need = !done && !parked && t.unit == NO_UNIT;
         const uint64_t needm = __ballot(need);
         if (needm) {
+            if (dbg) ++D.atomics;
             const int leader = __ffsll((unsigned long long)needm) - 1;
-            unsigned base = 0;
-            if (lane == leader) base = atomicAdd(P.queue, (unsigned)__popcll(needm));
-            base = __shfl(base, leader);
-            if (need) {
-                const unsigned u = base + (unsigned)__popcll(needm & below);
-                if (u >= P.nunits) {
-                    result = ST_DONE;
-                } else if (decode_unit(P, u).valid) {
-                    t.unit = u;
-                    t.i = (unsigned)(decode_unit(P, u).c * P.chunk);
-                    t.in_path = false;
-                    t.acc = mk(0, 0, 0);
-                }
-            }
-        }
-        if (result < 0 && t.unit != NO_UNIT) {
-            const Unit u = decode_unit(P, t.unit);
-            const unsigned c1 = (unsigned)min((u.c + 1) * P.chunk, P.spp);
-            smp.X = t.X;
-            while (true) {
-                if (!t.in_path) {
-                    if (t.i == c1) {
-                        store_partial(P, u, t.acc);
-                        t.unit = NO_UNIT;
+            const int k = __popcll(needm);
+            int h = 0, got = 0, ex = 0;
+            if (lane == leader) {  /* take up to k units from the workgroup's ring */
+                ex = __hip_atomic_load(&sh.exhausted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                h = lds_peek(&sh.uhead);
+                while (true) {
+                    const int avail =
+                        __hip_atomic_load(&sh.utail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - h;
+                    got = min(k, avail);
+                    if (got <= 0) {
+                        got = 0;
                         break;
                     }
-                    smp.X = vpt_stream_start(P.seed, u.idx, (uint64_t)t.i);
-                    ++t.i;
-                    t.p.o = o0;
-                    t.p.d = pool_camera_dir(P, smp, u.x, u.y);
+                    if (__hip_atomic_compare_exchange_strong(&sh.uhead, &h, h + got, __ATOMIC_ACQUIRE,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                        break;
+                }
+            }
+            h = __shfl(h, leader);
+            got = __shfl(got, leader);
+            ex = __shfl(ex, leader);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (need) {
+                const int r = __popcll(needm & below);
+                if (r >= got) {
+                    /* ring empty: retire only once the queue is exhausted (the flag was read before
+                     * utail, so no unit can still be on its way in); otherwise back to ring A */
+                    if (ex) done = true;
+                    else parked = true;
+                } else {
+                    const unsigned u = sh.uring[(h + r) % URING];
+                    const Unit uu = decode_unit(P, u);
+                    if (uu.valid) {  /* (an invalid unit -- a tile's padding -- is dropped) */
+                        t.unit = u;
+                        t.pix = (unsigned)uu.x | ((unsigned)uu.y << 16);
+                        t.i = (unsigned)(uu.c * P.chunk);
+                        t.c1 = (unsigned)min((uu.c + 1) * P.chunk, P.spp);
+                        t.in_path = false;
+                        t.acc = mk(0, 0, 0);
+                    }
+                }
+            }
+        }
+        const unsigned long long g1 = dbg_clock(dbg);
+        if (!done && !t.in_path && t.unit != NO_UNIT) {
+            if (t.i == t.c1) {
+                store_partial(P, decode_unit(P, t.unit), t.acc);
+                t.unit = NO_UNIT;
+            } else {
+                const int x = (int)(t.pix & 0xFFFFu), y = (int)(t.pix >> 16);
+                const uint64_t idx = (uint64_t)(P.h - 1 - y) * (uint64_t)P.w + (uint64_t)x;  /* src/rt.cpp:773 */
+                smp.X = vpt_stream_start(P.seed, idx, (uint64_t)t.i);
+                ++t.i;
+                if (dbg) ++D.samples;
+                const double jx = smp.next();  /* src/rt.cpp:787, x draw first */
+                const double jy = smp.next();
+                t.p.depth = 0;
+                if (continue_path(smp, t.p, m)) {
+                    t.p.o = mk(P.o[0], P.o[1], P.o[2]);
+                    t.p.d = pool_camera_dir(P, jx, jy, x, y);
                     t.p.beta = mk(1, 1, 1);
                     t.p.L = mk(0, 0, 0);
-                    t.p.depth = 0;
                     t.in_path = true;
+                    t.X = smp.X;
                 }
-                if (!continue_path(smp, t.p, m)) {
-                    t.acc = add(t.p.L, t.acc);  /* src/rt.cpp:794 */
-                    t.in_path = false;
-                    continue;
-                }
-                const int ev = decide<EST>(S, smp, t.p, t.e, m);
-                if (ev == EV_END) {
-                    t.acc = add(t.p.L, t.acc);
-                    t.in_path = false;
-                    continue;
-                }
-                result = ev == EV_SURF ? ST_S : ST_M;
-                break;
             }
-            t.X = smp.X;
         }
-        if (__ballot(result < 0) == 0) break;
+        if (dbg) {
+            D.c_g += g1 - g0;
+            D.c_s += dbg_clock(dbg) - g1;
+        }
+        if (__ballot(!done && !parked && !t.in_path) == 0) break;
+    }
+    const unsigned long long c1 = dbg_clock(dbg);
+    int result = parked ? ST_A : ST_DONE;
+    if (!done && !parked) {
+        if (dbg) ++D.lane_it;
+        smp.X = t.X;
+        const int ev = decide<EST>(S, smp, t.p, t.e, m);
+        t.X = smp.X;
+        if (ev == EV_END) {
+            t.acc = add(t.p.L, t.acc);
+            t.in_path = false;
+            result = ST_A;
+        } else {
+            result = ev == EV_SURF ? ST_S : ST_M;
+        }
+    }
+    if (dbg) {
+        D.c_grab += c1 - c0;
+        D.c_decide += dbg_clock(dbg) - c1;
     }
     return result;
 }
@@ -246,6 +324,7 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
         sh.tail[ST_S] = sh.tail[ST_M] = 0;
         sh.done = 0;
         sh.ticket = sh.serving = 0;
+        sh.uhead = sh.utail = sh.exhausted = 0;
     }
     __syncthreads();
 
@@ -256,6 +335,10 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
     smp.cnt.iterations = 0;
     int n = 0, slot = 0, next = ST_A;
     unsigned long long st_batches[3] = {0, 0, 0}, st_lanes[3] = {0, 0, 0}, st_idle = 0, st_retry = 0;
+    unsigned long long st_cyc[4] = {0, 0, 0, 0}, st_ls = 0;
+    ADbg D = {};
+    const bool dbg = stats != nullptr;
+    unsigned long long tclk = dbg ? __builtin_amdgcn_s_memtime() : 0;
     while (true) {
         /* ---- an idle wave waits outside the lock until some ring has work (racy peek) ---- */
         if (n == 0) {
@@ -299,6 +382,24 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
             if (lane == 0 && md) sh.done += __popcll(md);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        /* keep the unit ring stocked: the queue atomic's latency is paid here once per 128 units
+         * instead of in every stage-A round (all waves on the chip contend for that address) */
+        if (!__builtin_amdgcn_readfirstlane(sh.exhausted) &&
+            __builtin_amdgcn_readfirstlane(sh.utail - lds_peek(&sh.uhead)) < UREFILL) {
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(P.queue, (unsigned)UREFILL);
+            base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
+            const unsigned left = base < P.nunits ? P.nunits - base : 0u;
+            const int nv = (int)(left < (unsigned)UREFILL ? left : (unsigned)UREFILL);
+            const int t0 = sh.utail;
+            for (int j = lane; j < nv; j += 64) sh.uring[(t0 + j) % URING] = base + (unsigned)j;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) {
+                __hip_atomic_store(&sh.utail, t0 + nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (left <= (unsigned)UREFILL)
+                    __hip_atomic_store(&sh.exhausted, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
         const int done = __builtin_amdgcn_readfirstlane(sh.done);
         int cnt[3];
 #pragma unroll
@@ -320,43 +421,69 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
-        if (stats) {
+        if (dbg) {
             st_batches[st] += 1;
             st_lanes[st] += (unsigned long long)take;
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            st_cyc[3] += now - tclk;
+            tclk = now;
         }
 
         /* ---- run one stage on the batch ---- */
         const bool active = lane < n;
         Task t;
         if (st == ST_A) {
+            const unsigned long long l0 = dbg_clock(dbg);
             if (active) load_task(sh, slot, t, true);
             else {
                 t.unit = NO_UNIT;
                 t.in_path = false;
+                t.killed = false;
             }
-            next = stage_a<EST>(P, S, m, smp, t, active, lane, below);
+            const unsigned long long l1 = dbg_clock(dbg);
+            next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbg, D);
+            const unsigned long long l2 = dbg_clock(dbg);
             if (active) store_task(sh, slot, t, true);
+            if (dbg) st_ls += (l1 - l0) + (dbg_clock(dbg) - l2);
         } else if (active) {
             load_task(sh, slot, t, false);
             smp.X = t.X;
             if (st == ST_S) surface_event<EST>(S, smp, t.p, t.e, m);
             else medium_event<EST>(S, smp, t.p, t.e, m);
+            t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
             t.X = smp.X;
             store_task(sh, slot, t, false);
             next = ST_A;
+        }
+        if (dbg) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            st_cyc[st] += now - tclk;
+            tclk = now;
         }
     }
     if (COUNT) {
         atomicAdd(&counters[0], (unsigned long long)smp.cnt.tests);
         atomicAdd(&counters[1], (unsigned long long)smp.cnt.iterations);
     }
-    if (stats && lane == 0) {  /* debug: [batches A S M, lanes A S M, idle polls, lock retries] */
+    if (dbg) {  /* per-lane and leader-accumulated counters: summed over all lanes */
+        atomicAdd(&stats[14], D.lane_it);
+        atomicAdd(&stats[15], D.samples);
+    }
+    if (dbg && lane == 0) {
         for (int T = 0; T < 3; ++T) {
             atomicAdd(&stats[T], st_batches[T]);
             atomicAdd(&stats[3 + T], st_lanes[T]);
         }
         atomicAdd(&stats[6], st_idle);
         atomicAdd(&stats[7], st_retry);
+        for (int T = 0; T < 4; ++T) atomicAdd(&stats[8 + T], st_cyc[T]);
+        atomicAdd(&stats[12], D.outer);
+        atomicAdd(&stats[16], D.c_grab);
+        atomicAdd(&stats[18], D.c_decide);
+        atomicAdd(&stats[17], D.c_g);
+        atomicAdd(&stats[20], D.c_s);
+        atomicAdd(&stats[21], D.atomics);
+        atomicAdd(&stats[19], st_ls);
     }
 }
 
