@@ -398,6 +398,7 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
     int blocks = 0;
     int rc;
     if (!env_int("VPT_WAVE_KERNEL", 0)) {  /* default: workgroup task pool (vpt_pool.h) */
+        if (K.w > 65535 || K.h > 65535) return vpt_fail(VPT_E_INVALID, "width and height must be < 65536");
         PoolParams Q;
         Q.w = K.w;
         Q.h = K.h;
@@ -546,6 +547,8 @@ int vpt_set_scene(vpt_context* ctx, const vpt_sphere* s, int n)
         h.geo[i].r2 = q.r * q.r;
         h.geo[i].mat3 = q.material == 3;
         h.geo[i].emitter = (q.radiance[0] > 0 || q.radiance[1] > 0 || q.radiance[2] > 0);
+        h.geo[i].skey = q.material == 0 ? 0 : q.material == 1 ? 2 : 3;
+        h.geo[i].point = q.r == 0;
         if (h.geo[i].emitter) h.emit[h.n_emit++] = i;
         if (q.r > 0 && q.radiance[0] > 0) h.mis_light[h.n_mis++] = i;
         if (q.material == 3) h.n_mat3++;

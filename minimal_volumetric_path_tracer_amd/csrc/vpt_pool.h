@@ -5,14 +5,18 @@
  * radiance, chunk sum, erand48 state, pending event) lives in LDS, not in a lane.  A path loop
  * iteration of the reference (include/vptShadeMethods.h:1278-1336 / :1345-1481) is split into three
  * stages:
- *     A  roulette + intersection + light pick + distance sample   (decide(), vpt_device.h)
- *     S  surface event: pLight + MISv2 + bdsf                      (surface_event())
- *     M  medium event: single scattering + phase sample            (medium_event())
- * Each stage keeps a ring of task slots.  A wave takes the lock, returns its finished tasks to the
- * rings of their next stage, takes up to 64 tasks of the fullest stage, releases the lock, loads
- * those states, runs that ONE stage with (nearly) every lane busy, and stores the states back.  The
- * pool is larger than the workgroup (POOL > 256), so there is nearly always a full batch of some
- * stage: no wave runs a block with half its lanes idle, and no wave waits for its longest path.
+ *     A  intersection + light pick + distance sample   (decide(), vpt_device.h)
+ *     S  surface event: pLight + MISv2 + bdsf           (surface_event()) + next roulette draw
+ *     M  medium event: single scattering + phase sample (medium_event())  + next roulette draw
+ * Pending tasks wait in rings keyed by what their next stage will branch on, so that a batch runs
+ * one side of the divergent code only:
+ *     ring 0     stage A
+ *     ring 1..4  stage S: diffuse surface + sphere light, diffuse + point light, metal, other
+ *     ring 5..6  stage M: sphere light, point light
+ * A wave takes the workgroup's ticket lock, returns its finished tasks to the rings of their next
+ * stage, takes up to 64 tasks of the fullest ring, releases the lock, loads those states, runs
+ * that ONE stage with (nearly) every lane busy, and stores the states back.  The pool is larger
+ * than the workgroup (POOL > 256), so there is nearly always a full batch of some ring.
  *
  * Determinism: a task runs its unit's samples strictly in order and adds each sample to the
  * chunk sum as the reference adds to its pixel (acc = L + acc, src/rt.cpp:794); chunk sums are
@@ -27,37 +31,36 @@
 
 namespace vpt {
 
-constexpr int POOL = 448;        /* task slots per workgroup (256 lanes) -- ~76 KB of LDS, 2 WGs/CU */
-constexpr int NF = 18;           /* doubles per task */
-constexpr unsigned NO_UNIT = 0xFFFFFFFFu;
-constexpr int URING = 256, UREFILL = 128;  /* per-workgroup work-unit ring: one global atomic per 128 units */
-/* debug statistics (VPT_POOL_STATS=1, vpt_debug_pool_stats): [0-2] batches A/S/M, [3-5] lanes
- * A/S/M, [6] idle polls, [7] ticket waits, [8-10] cycles in stage A/S/M, [11] cycles scheduling,
- * [12] stage-A preparation rounds, [14] decide() calls (lanes), [15] samples started */
-constexpr int NSTATS = 24;  /* [16] stage-A cycles in the preparation loop, [18] in decide,
-                               [19] task load/store */
+constexpr int POOL = 440;   /* task slots per workgroup (256 lanes): 81 KB of LDS, 2 workgroups/CU */
+constexpr int NF = 18;      /* doubles per task */
+constexpr int NR = 7;       /* rings */
+constexpr int R_A = 0, R_S = 1, R_M = 5, R_DONE = NR;
+constexpr int URING = 256, UREFILL = 128;  /* work-unit ring: one global queue atomic per 128 units */
+
+/* debug statistics (VPT_POOL_STATS=1, vpt_debug_pool_stats): [0-6] batches per ring, [7-13] lanes
+ * per ring, [14] idle polls, [15] ticket waits, [16-19] cycles in stage A/S/M/scheduling, [20]
+ * stage-A preparation rounds, [21] samples started, [22] cycles preparing, [23] cycles in decide */
+constexpr int NSTATS = 24;
 struct ADbg {
-    unsigned long long outer, lane_it, samples;
-    unsigned long long c_grab, c_decide, c_g, c_s, atomics;
+    unsigned long long rounds, samples, c_prep, c_decide;
 };
 __device__ __forceinline__ unsigned long long dbg_clock(bool dbg) { return dbg ? __builtin_amdgcn_s_memtime() : 0; }
-enum { ST_A = 0, ST_S = 1, ST_M = 2, ST_DONE = 3 };
+
 enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_BX, F_BY, F_BZ, F_LX, F_LY, F_LZ, F_AX, F_AY, F_AZ, F_T, F_DIST,
        F_PDF };
 
 struct TaskPool {
-    double f[NF][POOL];     /* SoA: one array per field */
-    uint64_t X[POOL];       /* erand48 state */
-    uint32_t unit[POOL];    /* work unit, NO_UNIT when the task needs a new one */
-    uint32_t pix[POOL];     /* x | camera row << 16 */
-    uint32_t c1[POOL];      /* one past the unit's last sample */
-    uint32_t samp[POOL];    /* next sample to start | in_path << 31 */
-    uint32_t evw[POOL];     /* depth | id << 16 | src << 24 */
-    uint16_t ring[3][POOL]; /* slots waiting for stage A / S / M */
-    int head[3], tail[3];   /* monotonic ring counters */
-    int done;               /* slots retired (work queue exhausted) */
-    int ticket, serving;    /* FIFO ticket lock: a wave returning tasks is never starved */
-    uint32_t uring[URING];  /* prefetched work units (refilled under the lock, taken by CAS on uhead) */
+    double f[NF][POOL];      /* SoA: one array per field */
+    uint64_t X[POOL];        /* erand48 state */
+    uint32_t pix[POOL];      /* x | camera row << 16 of the unit's pixel */
+    uint32_t c1[POOL];       /* one past the unit's last sample; 0 = no unit */
+    uint32_t samp[POOL];     /* next sample to start | in_path << 31 */
+    uint32_t evw[POOL];      /* depth | id << 16 | src << 24 | killed << 31 */
+    uint16_t ring[NR][POOL]; /* slots waiting, per ring */
+    int head[NR], tail[NR];  /* monotonic ring counters */
+    int done;                /* slots retired (work queue exhausted) */
+    int ticket, serving;     /* FIFO ticket lock: a wave returning tasks is never starved */
+    uint32_t uring[URING];   /* prefetched work units (refilled under the lock, taken by CAS on uhead) */
     int uhead, utail, exhausted;
 };
 
@@ -77,10 +80,9 @@ struct PoolParams {
     unsigned* queue;
 };
 
-/* work unit -> pixel (8x8 tile order: a batch of 64 consecutive units is one tile, one chunk) */
+/* work unit -> pixel (8x8 tile order: 64 consecutive units are one tile, one chunk) */
 struct Unit {
-    int x, lr, y, c;
-    uint64_t idx;
+    int x, y, c;
     bool valid;
 };
 
@@ -92,12 +94,11 @@ __device__ __forceinline__ Unit decode_unit(const PoolParams& P, unsigned u)
     r.c = (int)(rem >> 6);
     const unsigned p = rem & 63u;
     r.x = (int)(tile % (unsigned)P.tiles_x) * 8 + (int)(p & 7u);
-    r.lr = (int)(tile / (unsigned)P.tiles_x) * 8 + (int)(p >> 3);
-    r.valid = r.x < P.w && r.lr < P.rows;
-    const int k = r.lr / P.band_rows, rr = r.lr - k * P.band_rows;
+    const int lr = (int)(tile / (unsigned)P.tiles_x) * 8 + (int)(p >> 3);  /* row within the shard */
+    r.valid = r.x < P.w && lr < P.rows;
+    const int k = lr / P.band_rows, rr = lr - k * P.band_rows;
     const int fr = (P.band_offset + k * P.band_stride) * P.band_rows + rr;  /* file row */
     r.y = P.h - 1 - fr;                                                       /* camera row */
-    r.idx = (uint64_t)fr * (uint64_t)P.w + (uint64_t)r.x;                     /* src/rt.cpp:773 */
     return r;
 }
 
@@ -119,9 +120,8 @@ struct Task {
     Event e;
     dv3 acc;
     uint64_t X;
-    unsigned unit;   /* work unit, NO_UNIT when the task needs one */
-    unsigned pix;    /* x | camera row << 16 of the unit's pixel */
-    unsigned c1;     /* one past the unit's last sample */
+    unsigned pix;    /* x | camera row << 16 */
+    unsigned c1;     /* one past the unit's last sample; 0 = the task needs a unit */
     unsigned i;      /* next sample to start */
     bool in_path, killed;
 };
@@ -143,7 +143,6 @@ __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bo
     t.X = sh.X[s];
     if (full) {
         t.acc = mk(sh.f[F_AX][s], sh.f[F_AY][s], sh.f[F_AZ][s]);
-        t.unit = sh.unit[s];
         t.pix = sh.pix[s];
         t.c1 = sh.c1[s];
         const uint32_t sm = sh.samp[s];
@@ -166,34 +165,39 @@ __device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, b
         sh.f[F_DIST][s] = t.e.dist;
         sh.f[F_PDF][s] = t.e.pdf;
         sh.f[F_AX][s] = t.acc.x; sh.f[F_AY][s] = t.acc.y; sh.f[F_AZ][s] = t.acc.z;
-        sh.unit[s] = t.unit;
         sh.pix[s] = t.pix;
         sh.c1[s] = t.c1;
         sh.samp[s] = t.i | (t.in_path ? 0x80000000u : 0u);
     }
 }
 
-__device__ __forceinline__ void store_partial(const PoolParams& P, const Unit& u, dv3 acc)
+/* the finished unit's chunk sum -> partials[shard row][x][chunk] */
+__device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t)
 {
-    const size_t o = (((size_t)u.lr * (size_t)P.w + (size_t)u.x) * (size_t)P.nch + (size_t)u.c) * 3;
-    P.partials[o] = acc.x;
-    P.partials[o + 1] = acc.y;
-    P.partials[o + 2] = acc.z;
+    const int x = (int)(t.pix & 0xFFFFu), y = (int)(t.pix >> 16);
+    const int fr = P.h - 1 - y;
+    const int k = fr / P.band_rows, rr = fr - k * P.band_rows;
+    const int lr = ((k - P.band_offset) / P.band_stride) * P.band_rows + rr;
+    const int c = (int)((t.c1 - 1u) / (unsigned)P.chunk);
+    const size_t o = (((size_t)lr * (size_t)P.w + (size_t)x) * (size_t)P.nch + (size_t)c) * 3;
+    P.partials[o] = t.acc.x;
+    P.partials[o + 1] = t.acc.y;
+    P.partials[o + 2] = t.acc.z;
 }
 
 /* Stage A for the lanes with `active`: at most ONE decide() per task.  A converged preparation
  * loop first gives every task a path that has survived its roulette draw.  Lanes that need a
- * work unit take them together (one queue atomic per round); a finished unit writes its chunk
+ * work unit take them together from the workgroup's unit ring; a finished unit writes its chunk
  * sum; a task without a path starts samples until one survives its first roulette draw.  A camera
  * sample killed by that draw has L = 0 and adds nothing to the sum (acc + 0 = acc exactly), so
  * only its three draws (jitter x, jitter y, roulette; src/rt.cpp:787 + vptShadeMethods.h:1282)
- * are taken and its camera ray is never built: the loop is ~100 integer/FP64 instructions a
- * round.  Then every ready lane runs decide() once; a path that ends there goes back to ring A.
- * Returns the task's next stage. */
+ * are taken and its camera ray is never built.  Then every ready lane runs decide() once; a path
+ * that ends there goes back to ring A.  Returns the ring of the task's next stage (R_DONE:
+ * retired). */
 template <int EST, bool COUNT>
-__device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const DevScene* __restrict__ S, const Medium& m,
-                                       Sampler<COUNT>& smp, Task& t, bool active, int lane, uint64_t below,
-                                       bool dbg, ADbg& D)
+__device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const DevScene* __restrict__ S,
+                                       const Medium& m, Sampler<COUNT>& smp, Task& t, bool active, int lane,
+                                       uint64_t below, bool dbg, ADbg& D)
 {
     bool done = !active, parked = false;
     if (active && t.killed) {  /* the S/M roulette ended the path */
@@ -203,12 +207,10 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
     }
     const unsigned long long c0 = dbg_clock(dbg);
     while (true) {
-        if (dbg) ++D.outer;
-        const unsigned long long g0 = dbg_clock(dbg);
-        const bool need = !done && !parked && t.unit == NO_UNIT;
+        if (dbg) ++D.rounds;
+        const bool need = !done && !parked && t.c1 == 0;
         const uint64_t needm = __ballot(need);
         if (needm) {
-            if (dbg) ++D.atomics;
             const int leader = __ffsll((unsigned long long)needm) - 1;
             const int k = __popcll(needm);
             int h = 0, got = 0, ex = 0;
@@ -240,10 +242,8 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                     if (ex) done = true;
                     else parked = true;
                 } else {
-                    const unsigned u = sh.uring[(h + r) % URING];
-                    const Unit uu = decode_unit(P, u);
+                    const Unit uu = decode_unit(P, sh.uring[(h + r) % URING]);
                     if (uu.valid) {  /* (an invalid unit -- a tile's padding -- is dropped) */
-                        t.unit = u;
                         t.pix = (unsigned)uu.x | ((unsigned)uu.y << 16);
                         t.i = (unsigned)(uu.c * P.chunk);
                         t.c1 = (unsigned)min((uu.c + 1) * P.chunk, P.spp);
@@ -253,11 +253,10 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                 }
             }
         }
-        const unsigned long long g1 = dbg_clock(dbg);
-        if (!done && !t.in_path && t.unit != NO_UNIT) {
+        if (!done && !parked && !t.in_path && t.c1 != 0) {
             if (t.i == t.c1) {
-                store_partial(P, decode_unit(P, t.unit), t.acc);
-                t.unit = NO_UNIT;
+                store_partial(P, t);
+                t.c1 = 0;
             } else {
                 const int x = (int)(t.pix & 0xFFFFu), y = (int)(t.pix >> 16);
                 const uint64_t idx = (uint64_t)(P.h - 1 - y) * (uint64_t)P.w + (uint64_t)x;  /* src/rt.cpp:773 */
@@ -277,29 +276,27 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                 }
             }
         }
-        if (dbg) {
-            D.c_g += g1 - g0;
-            D.c_s += dbg_clock(dbg) - g1;
-        }
         if (__ballot(!done && !parked && !t.in_path) == 0) break;
     }
     const unsigned long long c1 = dbg_clock(dbg);
-    int result = parked ? ST_A : ST_DONE;
+    int result = parked ? R_A : R_DONE;
     if (!done && !parked) {
-        if (dbg) ++D.lane_it;
         smp.X = t.X;
         const int ev = decide<EST>(S, smp, t.p, t.e, m);
         t.X = smp.X;
         if (ev == EV_END) {
             t.acc = add(t.p.L, t.acc);
             t.in_path = false;
-            result = ST_A;
+            result = R_A;
+        } else if (ev == EV_SURF) {
+            const int sk = S->geo[t.e.id].skey;
+            result = R_S + (sk == 0 ? S->geo[t.e.src].point : sk);
         } else {
-            result = ev == EV_SURF ? ST_S : ST_M;
+            result = R_M + S->geo[t.e.src].point;
         }
     }
     if (dbg) {
-        D.c_grab += c1 - c0;
+        D.c_prep += c1 - c0;
         D.c_decide += dbg_clock(dbg) - c1;
     }
     return result;
@@ -313,15 +310,16 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
     const int tid = threadIdx.x, lane = tid & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     for (int j = tid; j < POOL; j += 256) {
-        sh.unit[j] = NO_UNIT;
+        sh.c1[j] = 0;
         sh.samp[j] = 0;
         sh.evw[j] = 0;
-        sh.ring[ST_A][j] = (uint16_t)j;
+        sh.ring[R_A][j] = (uint16_t)j;
+    }
+    if (tid < NR) {
+        sh.head[tid] = 0;
+        sh.tail[tid] = tid == R_A ? POOL : 0;
     }
     if (tid == 0) {
-        sh.head[0] = sh.head[1] = sh.head[2] = 0;
-        sh.tail[ST_A] = POOL;
-        sh.tail[ST_S] = sh.tail[ST_M] = 0;
         sh.done = 0;
         sh.ticket = sh.serving = 0;
         sh.uhead = sh.utail = sh.exhausted = 0;
@@ -333,21 +331,20 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
     smp.g = m.g;
     smp.cnt.tests = 0;
     smp.cnt.iterations = 0;
-    int n = 0, slot = 0, next = ST_A;
-    unsigned long long st_batches[3] = {0, 0, 0}, st_lanes[3] = {0, 0, 0}, st_idle = 0, st_retry = 0;
-    unsigned long long st_cyc[4] = {0, 0, 0, 0}, st_ls = 0;
+    int n = 0, slot = 0, next = R_A;
+    unsigned long long st_idle = 0, st_retry = 0, st_sched = 0;
     ADbg D = {};
     const bool dbg = stats != nullptr;
-    unsigned long long tclk = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long tclk = dbg_clock(dbg);
     while (true) {
         /* ---- an idle wave waits outside the lock until some ring has work (racy peek) ---- */
         if (n == 0) {
             bool fin = false;
             while (true) {
-                const int pend = __builtin_amdgcn_readfirstlane(
-                    (lds_peek(&sh.tail[0]) - lds_peek(&sh.head[0])) + (lds_peek(&sh.tail[1]) - lds_peek(&sh.head[1])) +
-                    (lds_peek(&sh.tail[2]) - lds_peek(&sh.head[2])));
-                if (pend > 0) break;
+                int pend = 0;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) pend += lds_peek(&sh.tail[r]) - lds_peek(&sh.head[r]);
+                if (__builtin_amdgcn_readfirstlane(pend) > 0) break;
                 if (__builtin_amdgcn_readfirstlane(lds_peek(&sh.done)) == POOL) {
                     fin = true;
                     break;
@@ -357,7 +354,7 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
             }
             if (fin) break;
         }
-        /* ---- critical section: return finished tasks, take a batch of the fullest stage ---- */
+        /* ---- critical section: return finished tasks, take a batch of the fullest ring ---- */
         int ticket = 0;
         if (lane == 0) {
             ticket = __hip_atomic_fetch_add(&sh.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -369,16 +366,16 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (n > 0) {
 #pragma unroll
-            for (int T = 0; T < 3; ++T) {
-                const bool mine = lane < n && next == T;
+            for (int r = 0; r < NR; ++r) {
+                const bool mine = lane < n && next == r;
                 const uint64_t msk = __ballot(mine);
                 if (msk) {
-                    const int base = sh.tail[T];
-                    if (mine) sh.ring[T][(base + __popcll(msk & below)) % POOL] = (uint16_t)slot;
-                    if (lane == 0) sh.tail[T] = base + __popcll(msk);
+                    const int base = sh.tail[r];
+                    if (mine) sh.ring[r][(base + __popcll(msk & below)) % POOL] = (uint16_t)slot;
+                    if (lane == 0) sh.tail[r] = base + __popcll(msk);
                 }
             }
-            const uint64_t md = __ballot(lane < n && next == ST_DONE);
+            const uint64_t md = __ballot(lane < n && next == R_DONE);
             if (lane == 0 && md) sh.done += __popcll(md);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -401,12 +398,16 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
             }
         }
         const int done = __builtin_amdgcn_readfirstlane(sh.done);
-        int cnt[3];
+        int st = 0, best = -1;
 #pragma unroll
-        for (int T = 0; T < 3; ++T) cnt[T] = __builtin_amdgcn_readfirstlane(sh.tail[T] - sh.head[T]);
-        int st = cnt[ST_M] >= cnt[ST_S] ? ST_M : ST_S;
-        if (cnt[ST_A] > cnt[st]) st = ST_A;
-        const int take = min(64, cnt[st]);
+        for (int r = 0; r < NR; ++r) {
+            const int c = __builtin_amdgcn_readfirstlane(sh.tail[r] - sh.head[r]);
+            if (c > best) {
+                best = c;
+                st = r;
+            }
+        }
+        const int take = min(64, best);
         if (take > 0) {
             const int h0 = sh.head[st];
             if (lane < take) slot = sh.ring[st][(h0 + lane) % POOL];
@@ -421,43 +422,42 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
-        if (dbg) {
-            st_batches[st] += 1;
-            st_lanes[st] += (unsigned long long)take;
-            const unsigned long long now = __builtin_amdgcn_s_memtime();
-            st_cyc[3] += now - tclk;
+        if (dbg) {  /* debug only: per-batch global atomics (no runtime-indexed private arrays) */
+            if (lane == 0) {
+                atomicAdd(&stats[st], 1ull);
+                atomicAdd(&stats[7 + st], (unsigned long long)take);
+            }
+            const unsigned long long now = dbg_clock(dbg);
+            st_sched += now - tclk;
             tclk = now;
         }
 
         /* ---- run one stage on the batch ---- */
         const bool active = lane < n;
         Task t;
-        if (st == ST_A) {
-            const unsigned long long l0 = dbg_clock(dbg);
+        const int stage = st == R_A ? 0 : st < R_M ? 1 : 2;
+        if (stage == 0) {
             if (active) load_task(sh, slot, t, true);
             else {
-                t.unit = NO_UNIT;
+                t.c1 = 0;
                 t.in_path = false;
                 t.killed = false;
             }
-            const unsigned long long l1 = dbg_clock(dbg);
             next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbg, D);
-            const unsigned long long l2 = dbg_clock(dbg);
             if (active) store_task(sh, slot, t, true);
-            if (dbg) st_ls += (l1 - l0) + (dbg_clock(dbg) - l2);
         } else if (active) {
             load_task(sh, slot, t, false);
             smp.X = t.X;
-            if (st == ST_S) surface_event<EST>(S, smp, t.p, t.e, m);
+            if (stage == 1) surface_event<EST>(S, smp, t.p, t.e, m);
             else medium_event<EST>(S, smp, t.p, t.e, m);
             t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
             t.X = smp.X;
             store_task(sh, slot, t, false);
-            next = ST_A;
+            next = R_A;
         }
         if (dbg) {
-            const unsigned long long now = __builtin_amdgcn_s_memtime();
-            st_cyc[st] += now - tclk;
+            const unsigned long long now = dbg_clock(dbg);
+            if (lane == 0) atomicAdd(&stats[16 + stage], now - tclk);
             tclk = now;
         }
     }
@@ -465,25 +465,16 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
         atomicAdd(&counters[0], (unsigned long long)smp.cnt.tests);
         atomicAdd(&counters[1], (unsigned long long)smp.cnt.iterations);
     }
-    if (dbg) {  /* per-lane and leader-accumulated counters: summed over all lanes */
-        atomicAdd(&stats[14], D.lane_it);
-        atomicAdd(&stats[15], D.samples);
-    }
-    if (dbg && lane == 0) {
-        for (int T = 0; T < 3; ++T) {
-            atomicAdd(&stats[T], st_batches[T]);
-            atomicAdd(&stats[3 + T], st_lanes[T]);
+    if (dbg) {
+        atomicAdd(&stats[21], D.samples);
+        if (lane == 0) {
+            atomicAdd(&stats[14], st_idle);
+            atomicAdd(&stats[15], st_retry);
+            atomicAdd(&stats[19], st_sched);
+            atomicAdd(&stats[20], D.rounds);
+            atomicAdd(&stats[22], D.c_prep);
+            atomicAdd(&stats[23], D.c_decide);
         }
-        atomicAdd(&stats[6], st_idle);
-        atomicAdd(&stats[7], st_retry);
-        for (int T = 0; T < 4; ++T) atomicAdd(&stats[8 + T], st_cyc[T]);
-        atomicAdd(&stats[12], D.outer);
-        atomicAdd(&stats[16], D.c_grab);
-        atomicAdd(&stats[18], D.c_decide);
-        atomicAdd(&stats[17], D.c_g);
-        atomicAdd(&stats[20], D.c_s);
-        atomicAdd(&stats[21], D.atomics);
-        atomicAdd(&stats[19], st_ls);
     }
 }
 

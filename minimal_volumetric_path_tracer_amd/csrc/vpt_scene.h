@@ -19,7 +19,8 @@ struct GeoSphere {
     double r2;          /* fl(r*r), exactly the product Sphere::intersect forms (Sphere.h:30) */
     int32_t mat3;       /* material == 3 (skipped by intersectVPT) */
     int32_t emitter;    /* any radiance channel > 0 (vptShadeMethods.h:1296) */
-    int32_t pad_[2];
+    int32_t skey;       /* surface-stage ring of the pool kernel: 0 diffuse, 2 metal, 3 other */
+    int32_t point;      /* r == 0: a point light (its NEE casts a shadow ray) */
 };
 
 struct DevScene {

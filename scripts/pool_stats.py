@@ -5,27 +5,24 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import minimal_volumetric_path_tracer_amd as vpt
 
 NSTATS = 24
+RINGS = ["A", "S dif/sph", "S dif/pt", "S metal", "S other", "M sph", "M pt"]
 t = vpt.Tracer(0)
-sizes = [(256, 256, 64), (1024, 1024, 64), (1024, 1024, 256)]
+sizes = [(1024, 1024, 256)]
 for w, h, spp in sizes:
     t0 = time.time()
     t.render(width=w, height=h, spp=spp)
     dt = time.time() - t0
-    s = list((ctypes.c_ulonglong * NSTATS)())
     buf = (ctypes.c_ulonglong * NSTATS)()
     vpt.lib().vpt_debug_pool_stats(buf)
     s = list(buf)
-    b, l, cyc = s[0:3], s[3:6], s[8:12]
-    tot = sum(cyc)
-    print(f"{w}x{h}x{spp}: {dt*1e3:.1f} ms {w*h*spp/dt/1e6:.1f} Ms/s")
-    print(f"  batches A/S/M {b} mean lanes {[round(l[i]/max(b[i],1),1) for i in range(3)]}"
-          f" idle polls {s[6]} ticket waits {s[7]}")
-    print(f"  cycle share A/S/M/sched {[round(c/max(tot,1),3) for c in cyc]}"
-          f"  cycles per batch A/S/M {[round(cyc[i]/max(b[i],1)) for i in range(3)]}")
-    print(f"  stage A: prep rounds/batch {s[12]/max(b[0],1):.2f} decide lanes/batch {s[14]/max(b[0],1):.1f}"
-          f" samples {s[15]} (expect {w*h*spp})")
-    print(f"  stage A cycles/batch: prep {s[16]/max(b[0],1):.0f} decide {s[18]/max(b[0],1):.0f}"
-          f" load+store {s[19]/max(b[0],1):.0f}")
-    r = max(s[12], 1)
-    print(f"  prep round: grab section {s[17]/r:.0f} cycles, sample-start section {s[20]/r:.0f} cycles,"
-          f" rounds with a queue atomic {s[21]/r:.3f}", flush=True)
+    b, l, cyc = s[0:7], s[7:14], s[16:20]
+    tot = max(sum(cyc), 1)
+    nA = max(b[0], 1)
+    print(f"{w}x{h}x{spp}: {dt*1e3:.1f} ms {w*h*spp/dt/1e6:.1f} Ms/s (instrumented)")
+    for r in range(7):
+        print(f"  ring {RINGS[r]:10s} batches {b[r]:9d} mean lanes {l[r]/max(b[r],1):5.1f}")
+    print(f"  cycle share A/S/M/sched {[round(c/tot, 3) for c in cyc]}  idle polls {s[14]} ticket waits {s[15]}")
+    sb, mb = max(sum(b[1:5]), 1), max(sum(b[5:7]), 1)
+    print(f"  cycles per batch A {cyc[0]/nA:.0f} S {cyc[1]/sb:.0f} M {cyc[2]/mb:.0f}")
+    print(f"  stage A: prep rounds/batch {s[20]/nA:.2f} prep cycles/batch {s[22]/nA:.0f}"
+          f" decide cycles/batch {s[23]/nA:.0f} samples {s[21]} (expect {w*h*spp})", flush=True)
