@@ -6,7 +6,8 @@ camera (src/rt.cpp:755-759) and homogeneous medium (sigma_a 0.001, sigma_s 0.009
 src/rt.cpp:794), free-flight estimator (iterativeVPTracerFree, include/vptShadeMethods.h:1263),
 1024 x 1024 pixels x 256 samples per pixel.  One step = one full image: every rank renders its
 row bands (interleaved 16-row bands, scaling "strong": the image is fixed, the work is split) with
-one launch of render_kernel, then the float32 strips are gathered to rank 0 over RCCL (N > 1).
+one launch of pool_kernel (+ the chunk-sum reduce_kernel), then the float32 strips are gathered to
+rank 0 over RCCL (N > 1).
 Inputs (the 1.4 KB scene) are resident in HBM before the timed region; nothing is skipped.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config ff|mis|dense] [--no-cpu]
@@ -75,24 +76,43 @@ def cpu_baseline(threads: int) -> dict:
             "sample": f"oracle restatement (per-sample streams), 1024x256x8 spp free-flight, {threads} threads"}
 
 
-def pmc_traffic(config: str, world: int):
-    """HBM bytes per launch of render_kernel from the committed rocprofv3 PMC passes of this same
-    command (profiles/<round>/pmc_render_kernel.json, scripts/pmc.sh): (2 * FETCH_SIZE +
-    WRITE_SIZE) * 1 KiB -- gfx950 FETCH_SIZE reports half of a streamed read (MI355X_MICROARCH.md,
-    HBM).  Counters cannot be read live without the profiler; None when no profile matches."""
+def pmc_profile(config: str, world: int):
+    """The committed rocprofv3 PMC summary of this same command for the dominant kernel
+    (profiles/<round>/pmc_pool_kernel.json, scripts/pmc.sh + scripts/pmc_summary.py), newest round
+    first.  Counters cannot be read live without the profiler; None when no profile matches."""
     if config != "ff" or world != 1:
         return None
     import glob
 
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_render_kernel.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_pool_kernel.json")), reverse=True):
         try:
-            d = json.load(open(f))
-            c = d["counters"]
-            best = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
-        except (OSError, KeyError, ValueError):
+            return json.load(open(f))
+        except (OSError, ValueError):
             continue
-    return best
+    return None
+
+
+def pmc_traffic(prof):
+    """HBM bytes per launch: (2 * FETCH_SIZE + WRITE_SIZE) * 1 KiB -- gfx950 FETCH_SIZE reports half
+    of a streamed read (MI355X_MICROARCH.md, HBM)."""
+    try:
+        c = prof["counters"]
+        return int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+    except (TypeError, KeyError):
+        return None
+
+
+def pmc_fp64_flop(prof):
+    """All FP64 VALU work per launch, from the same profile: (add + mul + 2 fma + trans) wave
+    instructions x 64 lanes x VALU lane utilisation (the FLOPS_FP64 counter is not usable on this
+    stack).  Reported beside the intersection-only roofline of SURVEY 8(d)."""
+    try:
+        c = prof["counters"]
+        ops = c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + 2 * c["SQ_INSTS_VALU_FMA_F64"] + \
+            c["SQ_INSTS_VALU_TRANS_F64"]
+        return ops * 64 * prof["derived"]["valu_lane_utilization"]
+    except (TypeError, KeyError):
+        return None
 
 
 def main() -> None:
@@ -176,6 +196,8 @@ def main() -> None:
     value = samples_step * args.steps / elapsed / 1e6
     launch_samples = rows * W * SPP
     achieved = launch_samples * FLOP_PER_TEST * T / (kern_ms * 1e-3) / 1e12
+    prof = pmc_profile(args.config, world)
+    full = pmc_fp64_flop(prof)
     if rank == 0:
         img = image.float().cpu().numpy()
         res = {
@@ -204,13 +226,17 @@ def main() -> None:
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
-                "traffic": pmc_traffic(args.config, world),
-                "kernel": "render_kernel<FF>",
+                "traffic": pmc_traffic(prof),
+                "kernel": f"pool_kernel<{'FF' if c['estimator'] == 'ff' else 'MIS'}> + reduce_kernel (one launch pair)",
                 "kernel_ms": round(kern_ms, 3),
                 "algorithmic": f"{FLOP_PER_TEST} FP64 flop x {T:.2f} ray-sphere tests per sample (SURVEY 8d) x "
                                f"{launch_samples} samples per launch",
+                "all_fp64_tflops": round(full / (kern_ms * 1e-3) / 1e12, 3) if full else None,
+                "all_fp64_frac": round(full / (kern_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4) if full else None,
                 "note": "FP64 compute roof: MI355X FP64 vector and FP64 matrix peaks are both 78.6 TFLOP/s (spec); "
-                        "the kernel runs on the FP64 VALU, no MFMA (no dense contraction exists)",
+                        "the kernel runs on the FP64 VALU, no MFMA (no dense contraction exists). achieved/frac "
+                        "count intersection flops only (SURVEY 8d); all_fp64_* count every FP64 VALU op of the "
+                        "kernel (committed PMC profile of this command, profiles/r*/pmc_pool_kernel.json)",
             },
             "image_mean": [round(float(x), 6) for x in img.reshape(-1, 3).mean(0)],
         }
