@@ -62,9 +62,13 @@ typedef struct vpt_ray {
 } vpt_ray;
 
 typedef enum {
-    VPT_FREE_FLIGHT = 0,       /* iterativeVPTracerFree, vptShadeMethods.h:1263 */
-    VPT_MIS_EQUIANGULAR = 1    /* MISVPTTracerRecursive, vptShadeMethods.h:1345 */
+    VPT_FREE_FLIGHT = 0,           /* iterativeVPTracerFree, vptShadeMethods.h:1263 (main's estimator) */
+    VPT_MIS_EQUIANGULAR = 1,       /* MISVPTTracerRecursive, vptShadeMethods.h:1345 */
+    VPT_EXPLICIT_FREE = 2,         /* explicitVPTracerRecursiveFree, vptShadeMethods.h:1153 */
+    VPT_IMPLICIT_FREE = 3,         /* implicitVPTracerRecursiveFree, vptShadeMethods.h:940 */
+    VPT_EXPLICIT_EQUIANGULAR = 4   /* explicitVPTracerRecursive, vptShadeMethods.h:1014 */
 } vpt_estimator;
+#define VPT_NUM_ESTIMATORS 5
 
 typedef enum {
     VPT_FB_F32 = 0,            /* framebuffer: 3 x float per pixel */

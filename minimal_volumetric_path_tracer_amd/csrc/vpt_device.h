@@ -699,29 +699,56 @@ VPT_DEV bool continue_path(Sampler<COUNT>& smp, const Path& p, const Medium& m)
     return !(smp.next() < q);
 }
 
-/* vptShadeMethods.h:1284-1307 (FF) / :1357-1426 (MIS): what happens to the path this iteration. */
+/* Estimators (EST = include/vpt.h vpt_estimator):
+ *   0 iterativeVPTracerFree          vptShadeMethods.h:1263   free flight, NEE, loop
+ *   1 MISVPTTracerRecursive          vptShadeMethods.h:1345   equi-angular, NEE, surface test exp(-σt t)
+ *   2 explicitVPTracerRecursiveFree  vptShadeMethods.h:1153   free flight, NEE, recursive sums
+ *   3 implicitVPTracerRecursiveFree  vptShadeMethods.h:940    free flight, no NEE, lights at any depth
+ *   4 explicitVPTracerRecursive      vptShadeMethods.h:1014   equi-angular, NEE, surface test Tr(x, xs)
+ * The recursive ones (1-4) are R = A + B*R'; they are evaluated front to back with a running
+ * throughput (same draws and branches; only the final sums are reassociated). */
+template <int EST>
+VPT_DEV constexpr bool est_free_flight() { return EST == 0 || EST == 2 || EST == 3; }
+
+/* vptShadeMethods.h:1284-1307 (FF), :1357-1426 (MIS), :1166-1205 (explicit free), :950-977
+ * (implicit free), :1031-1096 (explicit): what happens to the path this iteration. */
 template <int EST, bool COUNT>
 VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, Event& e, const Medium& m)
 {
     const double sigma_t = m.sigma_a + m.sigma_s;
     int id = 0;
     double t;
-    if (!scene_intersect(S, smp, p.o, p.d, t, id, false)) t = VPT_MAXFLOAT;
-    const int count = S->n_emit;
-    if (count == 0) return EV_END;
+    const bool hit = scene_intersect(S, smp, p.o, p.d, t, id, false);
+    if (!hit) t = VPT_MAXFLOAT;
     e.t = t;
     e.id = id;
+    if (EST == 3) {  /* implicit: no light pick; success pdf freeFlightProb(d) * (1 - Tr(x, xs)) */
+        const double TrActual = hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0;
+        e.src = 0;
+        e.dist = -vm_log(1 - smp.next()) / sigma_t;
+        e.pdf = (sigma_t * vm_exp(sigma_t * e.dist * -1.0)) * (1.0 - TrActual);  /* :977 */
+        if (!(e.dist > t)) return EV_MED;
+        if (S->geo[id].emitter) {  /* :978-980: a light returns its radiance at any depth */
+            p.L = add(p.L, mul(p.beta, sph_rad(S, id)));
+            return EV_END;
+        }
+        return EV_SURF;
+    }
+    const int count = S->n_emit;
+    if (count == 0) return EV_END;
     e.src = S->emit[(int)(smp.next() * count)];
     bool surf;
-    if (EST == 0) {
+    if (est_free_flight<EST>()) {
         e.dist = -vm_log(1 - smp.next()) / sigma_t;  /* freeFlightSample, vptSamplingFunctions.h:11-14 */
         surf = e.dist > t;
     } else {
         double D = 0, ta = 0, tb = 0, sd = 0;
-        double psurf = vm_exp(sigma_t * t * -1.0);
+        /* MIS: psurf = exp(-σt t) (:1419); explicit: TrActual = Tr(x, xs), 0 on a miss (:1033-1041) */
+        const double psurf = EST == 1 ? vm_exp(sigma_t * t * -1.0)
+                                      : (hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0);
         e.dist = equiangular_params2(S, smp, e.src, t, p.o, p.d, D, ta, tb, sd);
         e.pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
-        surf = smp.next() < psurf;
+        surf = EST == 1 ? smp.next() < psurf : smp.next() <= psurf;  /* :1423 / :1096 */
     }
     if (!surf) return EV_MED;
     if (S->geo[id].emitter) {  /* the path ends on a light; only a camera ray sees it */
@@ -738,10 +765,22 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
 {
     const double sigma_t = m.sigma_a + m.sigma_s;
     const double continueprob = 0.6;
-    const double probSource = 1.0 / S->n_emit;
     const int id = e.id, src = e.src;
     const dv3 xs = add(p.o, scl(p.d, e.t));
     const dv3 nx = nrm(sub(xs, sph_p(S, id)));
+    if (EST == 3) {  /* implicit: BSDF continuation only, vptShadeMethods.h:983-994 */
+        dv3 wi = mk(0, 0, 0);
+        double pdf = 0;
+        dv3 fs = bdsf(S, smp, wi, p.d, nx, pdf, id);
+        wi = nrm(wi);
+        const double cosine = dot(nx, wi);
+        p.beta = scl(scl(scl(mul(p.beta, fs), (1 / continueprob)), cosine), (1 / pdf));
+        p.o = xs;
+        p.d = wi;
+        p.depth++;
+        return;
+    }
+    const double probSource = 1.0 / S->n_emit;
     const double alpha = S->sph[id].alpha;
     double Trs = transmitance(xs, sph_p(S, src), sigma_t);
     dv3 Ldp = scl(scl(p_light(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
@@ -767,12 +806,27 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
     const double continueprob = 0.6;
-    const double probSource = 1.0 / S->n_emit;
     dv3 xt = add(p.o, scl(p.d, e.dist));
+    if (EST == 3) {  /* implicit: vptShadeMethods.h:1000-1006 */
+        const double T = transmitance(p.o, xt, sigma_t);
+        dv3 wi = phase_sample(smp, p.d);
+        p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / e.pdf));
+        p.d = wi;
+        p.o = xt;
+        p.depth++;
+        return;
+    }
+    const double probSource = 1.0 / S->n_emit;
     if (EST == 0) {
         dv3 Ld = single_scattering(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
         dv3 wi = phase_sample(smp, p.d);
         p.L = add(p.L, scl(scl(mul(Ld, p.beta), (sigma_s / sigma_t)), (1 / continueprob)));
+        p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
+        p.d = wi;
+    } else if (EST == 2) {  /* vptShadeMethods.h:1252-1258 */
+        dv3 Ld = single_scattering(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
+        dv3 wi = phase_sample(smp, p.d);
+        p.L = add(p.L, mul(p.beta, scl(scl(Ld, (sigma_s / sigma_t)), (1 / continueprob))));
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else {

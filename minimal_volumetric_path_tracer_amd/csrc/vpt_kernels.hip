@@ -311,7 +311,7 @@ static int check_medium(const vpt_medium* m)
         return vpt_fail(VPT_E_INVALID, "sigma_a/sigma_s must be finite and >= 0");
     if (!is_finite(m->hg_g) || m->hg_g <= -1.0 || m->hg_g >= 1.0) return vpt_fail(VPT_E_INVALID, "hg_g must be in (-1, 1)");
     if (m->max_depth < 0) return vpt_fail(VPT_E_INVALID, "max_depth must be >= 0");
-    if (m->estimator != VPT_FREE_FLIGHT && m->estimator != VPT_MIS_EQUIANGULAR)
+    if (m->estimator < 0 || m->estimator >= VPT_NUM_ESTIMATORS)
         return vpt_fail(VPT_E_INVALID, "unknown estimator %d", m->estimator);
     return VPT_OK;
 }
@@ -386,10 +386,15 @@ static int env_int(const char* name, int dflt)
 }
 
 template <int EST, bool COUNT, int FB>
+static int launch_wave(vpt_context* ctx, KParams K, hipStream_t stream);
+
+template <int EST, bool COUNT, int FB>
 static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
 {
     const DevScene* S = ctx->d_scene;
-    if (env_int("VPT_SIMPLE_KERNEL", 0)) {  /* A/B: one lane = one pixel, samples in sequence */
+    /* counting (vpt_count_work) needs only the totals: the one-lane-per-pixel kernel, which is
+     * also the A/B baseline (VPT_SIMPLE_KERNEL=1: samples in sequence per lane) */
+    if (COUNT || env_int("VPT_SIMPLE_KERNEL", 0)) {
         dim3 grid((unsigned)((K.w + 15) / 16), (unsigned)((K.shard_rows + 15) / 16));
         render_kernel_simple<EST, COUNT, FB><<<grid, dim3(256), 0, stream>>>(K, S);
         HIP_OK(hipGetLastError());
@@ -397,7 +402,8 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
     }
     int blocks = 0;
     int rc;
-    if (!env_int("VPT_WAVE_KERNEL", 0)) {  /* default: workgroup task pool (vpt_pool.h) */
+    const bool wave = EST <= 1 && env_int("VPT_WAVE_KERNEL", 0);  /* A/B: the previous design, FF/MIS */
+    if (!wave) {  /* default: workgroup task pool (vpt_pool.h) */
         if (K.w > 65535 || K.h > 65535) return vpt_fail(VPT_E_INVALID, "width and height must be < 65536");
         PoolParams Q;
         Q.w = K.w;
@@ -449,7 +455,16 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         HIP_OK(hipGetLastError());
         return VPT_OK;
     }
-    rc = persistent_grid(ctx, render_kernel<EST, COUNT, FB>, &blocks);
+    if constexpr (EST <= 1) return launch_wave<EST, COUNT, FB>(ctx, K, stream);
+    return VPT_OK;
+}
+
+template <int EST, bool COUNT, int FB>
+static int launch_wave(vpt_context* ctx, KParams K, hipStream_t stream)
+{
+    const DevScene* S = ctx->d_scene;
+    int blocks = 0;
+    int rc = persistent_grid(ctx, render_kernel<EST, COUNT, FB>, &blocks);
     if (rc) return rc;
     const int tiles = K.tiles_x * K.tiles_y;
     const int need = (tiles + 3) / 4;  /* 4 waves per block, one tile per wave to start */
@@ -470,12 +485,19 @@ static int launch_render(vpt_context* ctx, KParams K, hipStream_t stream)
     K.tiles_y = (K.shard_rows + 7) / 8;
     K.cost_surf = env_int("VPT_COST_SURF", 1);
     K.cost_med = env_int("VPT_COST_MED", 1);
-    if (K.est == VPT_FREE_FLIGHT) {
-        if (K.fb == VPT_FB_F32) return launch_one<0, COUNT, VPT_FB_F32>(ctx, K, stream);
-        return launch_one<0, COUNT, VPT_FB_F64>(ctx, K, stream);
+#define VPT_LAUNCH_EST(E)                                                              \
+    case E:                                                                            \
+        if (K.fb == VPT_FB_F32) return launch_one<E, COUNT, VPT_FB_F32>(ctx, K, stream); \
+        return launch_one<E, COUNT, VPT_FB_F64>(ctx, K, stream);
+    switch (K.est) {
+        VPT_LAUNCH_EST(0)
+        VPT_LAUNCH_EST(1)
+        VPT_LAUNCH_EST(2)
+        VPT_LAUNCH_EST(3)
+        VPT_LAUNCH_EST(4)
     }
-    if (K.fb == VPT_FB_F32) return launch_one<1, COUNT, VPT_FB_F32>(ctx, K, stream);
-    return launch_one<1, COUNT, VPT_FB_F64>(ctx, K, stream);
+#undef VPT_LAUNCH_EST
+    return vpt_fail(VPT_E_INVALID, "unknown estimator %d", K.est);
 }
 
 extern "C" {
@@ -646,10 +668,13 @@ int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, 
     if (e == hipSuccess) {
         Medium mm{m->sigma_a, m->sigma_s, m->hg_g, m->max_depth};
         dim3 grid((unsigned)((n + 255) / 256)), block(256);
-        if (m->estimator == VPT_FREE_FLIGHT)
-            trace_batch_kernel<0><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso);
-        else
-            trace_batch_kernel<1><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso);
+        switch (m->estimator) {
+        case 0: trace_batch_kernel<0><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        case 1: trace_batch_kernel<1><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        case 2: trace_batch_kernel<2><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        case 3: trace_batch_kernel<3><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        default: trace_batch_kernel<4><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        }
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpy(out_rgb, dout, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost);

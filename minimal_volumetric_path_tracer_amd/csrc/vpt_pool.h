@@ -288,11 +288,11 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             t.acc = add(t.p.L, t.acc);
             t.in_path = false;
             result = R_A;
-        } else if (ev == EV_SURF) {
+        } else if (ev == EV_SURF) {  /* (the implicit estimator, EST 3, picks no light) */
             const int sk = S->geo[t.e.id].skey;
-            result = R_S + (sk == 0 ? S->geo[t.e.src].point : sk);
+            result = R_S + (sk == 0 ? (EST == 3 ? 0 : S->geo[t.e.src].point) : sk);
         } else {
-            result = R_M + S->geo[t.e.src].point;
+            result = R_M + (EST == 3 ? 0 : S->geo[t.e.src].point);
         }
     }
     if (dbg) {

@@ -4,8 +4,9 @@ Reference (gabo99cas/minimal_volumetric_path_tracer):
   * scene: ``std::vector<Sphere> spheres`` (include/Sphere.h:49, include/Sphere.cpp:7-107) with
     ``Sphere(r, p, c, radiance, material, eta, kappa, alpha)`` (include/Sphere.h:23);
   * per-sample estimators ``iterativeVPTracerFree(ray, sigma_a, sigma_s)``
-    (include/vptShadeMethods.h:1263) and ``MISVPTTracerRecursive(ray, sigma_a, sigma_s, depth)``
-    (include/vptShadeMethods.h:1345), returning a Color;
+    (include/vptShadeMethods.h:1263, the one ``main`` calls), ``MISVPTTracerRecursive(ray, sigma_a,
+    sigma_s, depth)`` (:1345), ``explicitVPTracerRecursiveFree`` (:1153),
+    ``implicitVPTracerRecursiveFree`` (:940) and ``explicitVPTracerRecursive`` (:1014), returning a Color;
   * ``main`` (src/rt.cpp:744-830): camera, pixel loop, average, clamp, ``image.ppm``.
 
 Here the same names take batches and run through libvpt.so (HIP, gfx950).  Argument meaning is
@@ -22,9 +23,12 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import FB_F32, FB_F64, FREE_FLIGHT, MIS_EQUIANGULAR, RAY_DTYPE, SPHERE_DTYPE, check, lib
+from ._lib import (EXPLICIT_EQUIANGULAR, EXPLICIT_FREE, FB_F32, FB_F64, FREE_FLIGHT, IMPLICIT_FREE, MIS_EQUIANGULAR,
+                   RAY_DTYPE, SPHERE_DTYPE, check, lib)
 
-ESTIMATORS = {"ff": FREE_FLIGHT, "free_flight": FREE_FLIGHT, "mis": MIS_EQUIANGULAR, "mis_equiangular": MIS_EQUIANGULAR}
+ESTIMATORS = {"ff": FREE_FLIGHT, "free_flight": FREE_FLIGHT, "mis": MIS_EQUIANGULAR, "mis_equiangular": MIS_EQUIANGULAR,
+              "explicit_free": EXPLICIT_FREE, "implicit_free": IMPLICIT_FREE, "explicit": EXPLICIT_EQUIANGULAR,
+              "explicit_equiangular": EXPLICIT_EQUIANGULAR}
 
 
 def Sphere(r, p, c=(0, 0, 0), radiance=(0, 0, 0), material=0, eta=(0, 0, 0), kappa=(0, 0, 0), alpha=0.0) -> np.ndarray:
@@ -166,6 +170,18 @@ class Tracer:
     def MISVPTTracerRecursive(self, rays, states, sigma_a=0.001, sigma_s=0.009, **kw):
         """Batched include/vptShadeMethods.h:1345 (depth 0)."""
         return self.trace("mis", rays, states, sigma_a, sigma_s, **kw)
+
+    def explicitVPTracerRecursiveFree(self, rays, states, sigma_a=0.001, sigma_s=0.009, **kw):
+        """Batched include/vptShadeMethods.h:1153 (depth 0)."""
+        return self.trace("explicit_free", rays, states, sigma_a, sigma_s, **kw)
+
+    def implicitVPTracerRecursiveFree(self, rays, states, sigma_a=0.001, sigma_s=0.009, **kw):
+        """Batched include/vptShadeMethods.h:940."""
+        return self.trace("implicit_free", rays, states, sigma_a, sigma_s, **kw)
+
+    def explicitVPTracerRecursive(self, rays, states, sigma_a=0.001, sigma_s=0.009, **kw):
+        """Batched include/vptShadeMethods.h:1014 (depth 0)."""
+        return self.trace("explicit", rays, states, sigma_a, sigma_s, **kw)
 
     def math_probe(self, fn: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float64)

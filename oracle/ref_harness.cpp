@@ -98,15 +98,31 @@ void ref_set_scene(const void* in, int n)
     spheres = v;
 }
 
-/* One camera sample through an estimator: 0 = iterativeVPTracerFree (vptShadeMethods.h:1263),
- * 1 = MISVPTTracerRecursive (vptShadeMethods.h:1345).  `state` is the erand48 state before the
- * call; the state after the call is returned (tells how many draws were consumed). */
+/* The reference's estimators by the build's numbering (include/vpt.h vpt_estimator):
+ *   0 iterativeVPTracerFree          vptShadeMethods.h:1263
+ *   1 MISVPTTracerRecursive          vptShadeMethods.h:1345
+ *   2 explicitVPTracerRecursiveFree  vptShadeMethods.h:1153
+ *   3 implicitVPTracerRecursiveFree  vptShadeMethods.h:938
+ *   4 explicitVPTracerRecursive      vptShadeMethods.h:1014 */
+static Color run_estimator(int estimator, const Ray& r, double sa, double ss)
+{
+    switch (estimator) {
+    case 0: return iterativeVPTracerFree(r, sa, ss);
+    case 1: return MISVPTTracerRecursive(r, sa, ss, 0);
+    case 2: return explicitVPTracerRecursiveFree(r, sa, ss, 0);
+    case 3: return implicitVPTracerRecursiveFree(r, sa, ss);
+    default: return explicitVPTracerRecursive(r, sa, ss, 0);
+    }
+}
+
+/* One camera sample through an estimator.  `state` is the erand48 state before the call; the
+ * state after the call is returned (tells how many draws were consumed). */
 uint64_t ref_trace(int estimator, const double ray[6], uint64_t state, double sa, double ss,
                    double out[3])
 {
     set_state(state);
     Ray r(V(ray), V(ray + 3));
-    Color c = estimator == 0 ? iterativeVPTracerFree(r, sa, ss) : MISVPTTracerRecursive(r, sa, ss, 0);
+    Color c = run_estimator(estimator, r, sa, ss);
     put(c, out);
     return get_state();
 }
@@ -130,9 +146,7 @@ void ref_render(int w, int h, int spp, int estimator, double sa, double ss, uint
                 double jy = erand48(seed);
                 Vector cameraRayDir = cx * ((static_cast<double>(x) + jx - 0.5) / w - .5) +
                                       cy * ((static_cast<double>(y) + jy - 0.5) / h - .5) + camera.d;
-                Color L = estimator == 0
-                              ? iterativeVPTracerFree(Ray(camera.o, cameraRayDir.normalize()), sa, ss)
-                              : MISVPTTracerRecursive(Ray(camera.o, cameraRayDir.normalize()), sa, ss, 0);
+                Color L = run_estimator(estimator, Ray(camera.o, cameraRayDir.normalize()), sa, ss);
                 if (per_sample) put(L, per_sample + ((size_t)idx * spp + i) * 3);
                 pixelValue = L + pixelValue;
             }

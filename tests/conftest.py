@@ -38,6 +38,12 @@ def samples():
 
 
 @pytest.fixture(scope="session")
+def samples_e234():
+    """per-sample KATs + framebuffers of estimators 2-4 (tests/golden/make_golden.py --estimators-234)"""
+    return dict(np.load(os.path.join(GOLDEN, "samples_e234.npz")))
+
+
+@pytest.fixture(scope="session")
 def prims():
     return dict(np.load(os.path.join(GOLDEN, "primitives.npz")))
 

@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(HERE))
 
 from oracle.oracle import Reference  # noqa: E402
-from scenes import SCENES, stream_state  # noqa: E402
+from scenes import EST_SCENES, SCENES, stream_state  # noqa: E402
 
 SEED = 0x5EED0001
 W = H = 64
@@ -217,5 +217,30 @@ def main():
     print("wrote fixtures to", HERE)
 
 
+def estimators_234():
+    """Per-sample known answers and 24x24x4 framebuffers of the other three estimators
+    (explicitVPTracerRecursiveFree, implicitVPTracerRecursiveFree, explicitVPTracerRecursive;
+    include/vptShadeMethods.h:1153, :940, :1014) -> samples_e234.npz.  Own RNG seed, so the
+    estimator 0/1 fixtures above stay byte-identical."""
+    ref = Reference()
+    rng = np.random.default_rng(20261015)
+    bundle = {}
+    for name, mk in EST_SCENES.items():
+        sc = mk()
+        ref.set_scene(sc)
+        bundle[f"{name}__scene"] = sc.view(np.uint8)
+        for est in (2, 3, 4):
+            ps = per_sample(ref, est, 384, rng)
+            for k, v in ps.items():
+                bundle[f"{name}__e{est}__{k}"] = v
+            bundle[f"{name}__e{est}__fb24x24x4"] = ref.render(24, 24, 4, est, seed=SEED)
+    np.savez_compressed(os.path.join(HERE, "samples_e234.npz"), **bundle)
+    print("wrote", os.path.join(HERE, "samples_e234.npz"))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--estimators-234"]:
+        estimators_234()
+    else:
+        main()
+        estimators_234()

@@ -72,6 +72,14 @@ def no_emitter_scene():
     return np.concatenate([s[:7]])
 
 
+def big_light_scene():
+    """default scene with an emissive ceiling (a 1e5-radius emitter): paths hit a light often, so
+    the implicit estimator (which only scores on a light hit) is exercised."""
+    s = default_scene()
+    s[4]["radiance"] = (4.0, 4.0, 3.0)
+    return s
+
+
 SCENES = {
     "default": default_scene,
     "dielectric": dielectric_scene,
@@ -79,6 +87,9 @@ SCENES = {
     "point_lights": point_lights_scene,
     "no_emitter": no_emitter_scene,
 }
+
+# scenes of the estimator fixtures (tests/golden/samples_e234.npz)
+EST_SCENES = dict(SCENES, big_light=big_light_scene)
 
 
 # independent (pure Python) statement of the per-sample stream spec (csrc/vpt_rng.h)

@@ -237,3 +237,78 @@ def test_full_size_properties(gpu_tracer, orc_vm):
     m, ms = img.reshape(-1, 3).mean(0), small.reshape(-1, 3).mean(0)
     se = np.sqrt(img.reshape(-1, 3).var(0) * 8 / img.size * 3 + small.reshape(-1, 3).var(0) * 16 / small.size * 3)
     assert np.all(np.abs(m - ms) <= 6 * se + 1e-6), (m, ms, se)
+
+
+# ---------------------------------------------------------------- estimators 2-4
+# explicitVPTracerRecursiveFree (2), implicitVPTracerRecursiveFree (3), explicitVPTracerRecursive
+# (4): include/vptShadeMethods.h:1153, :940, :1014.
+from scenes import EST_SCENES  # noqa: E402
+
+EST234 = {2: "explicit_free", 3: "implicit_free", 4: "explicit"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", list(EST_SCENES))
+@pytest.mark.parametrize("est", [2, 3, 4])
+def test_trace_batch_vs_oracle_bitwise_e234(gpu_tracer, orc_vm, samples_e234, scene, est):
+    sc = samples_e234[f"{scene}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    k = f"{scene}__e{est}__"
+    rays, st = samples_e234[k + "ray"], samples_e234[k + "state1"]
+    L, s = gpu_tracer.trace(EST234[est], _rays(rays), st)
+    Lo, so = orc_vm.trace(est, rays, st)
+    assert np.array_equal(s, so)
+    same = bitwise_equal(L, Lo)
+    assert same.all(), f"{(~same.all(1)).sum()} of {len(L)} samples differ"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["default", "big_light", "dielectric"])
+@pytest.mark.parametrize("est", [2, 3, 4])
+def test_trace_batch_vs_reference_e234(gpu_tracer, samples_e234, scene, est):
+    """against the reference's own per-sample values (same statistics bar as estimators 0/1)"""
+    sc = samples_e234[f"{scene}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    k = f"{scene}__e{est}__"
+    L, s = gpu_tracer.trace(est, _rays(samples_e234[k + "ray"]), samples_e234[k + "state1"])
+    ref = samples_e234[k + "L"]
+    assert (s == samples_e234[k + "state2"]).mean() >= 0.97
+    close = bitwise_equal(L, ref) | (np.abs(L - ref) <= 1e-9 * np.maximum(np.abs(ref), 1e-12))
+    assert close.all(1).mean() >= 0.88
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["default", "big_light"])
+@pytest.mark.parametrize("est", [2, 3, 4])
+def test_render_vs_oracle_bitwise_e234(gpu_tracer, orc_vm, scene, est):
+    sc = EST_SCENES[scene]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    g = gpu_tracer.render(width=40, height=28, spp=20, estimator=EST234[est], seed=SEED, fp64=True)
+    o = orc_vm.render(40, 28, 20, est, seed=SEED)
+    assert bitwise_equal(g, o).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("g,depth", [(0.5, 0), (0.0, 3)])
+@pytest.mark.parametrize("est", [2, 3, 4])
+def test_extensions_vs_oracle_e234(gpu_tracer, orc_vm, g, depth, est):
+    sc = EST_SCENES["big_light"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    gp = gpu_tracer.render(width=24, height=16, spp=4, estimator=est, hg_g=g, max_depth=depth, sigma_a=0.01,
+                           sigma_s=0.09, seed=3, fp64=True)
+    o = orc_vm.render(24, 16, 4, est, hg_g=g, max_depth=depth, sigma_a=0.01, sigma_s=0.09, seed=3)
+    assert bitwise_equal(gp, o).all()
+
+
+@pytest.mark.gpu
+def test_count_work_matches_oracle_e234(gpu_tracer, orc_vm):
+    sc = EST_SCENES["big_light"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    for est in (2, 3, 4):
+        t, it = gpu_tracer.count_work(vpt.RenderConfig(width=32, height=24, spp=4, estimator=est, seed=9))
+        _, c = orc_vm.render(32, 24, 4, est, seed=9, counters=True)
+        assert (t, it) == (c.tests, c.iterations)

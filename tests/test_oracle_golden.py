@@ -187,3 +187,45 @@ def test_primitives_media(orc, prims):
 def test_to_display(orc, prims):
     got = [orc.prim("to_display")(v) for v in prims["disp_in"]]
     assert np.array_equal(got, prims["to_display"])
+
+
+# ---- the other estimators: explicitVPTracerRecursiveFree (2),
+# implicitVPTracerRecursiveFree (3), explicitVPTracerRecursive (4), include/vptShadeMethods.h:1153,
+# :940, :1014.  All recursive: same draws bit-for-bit, values within 1e-12 relative (H14).
+from scenes import EST_SCENES  # noqa: E402
+
+
+def _close_nan_aware(out, ref, rtol=1e-12):
+    assert np.array_equal(np.isnan(ref), np.isnan(out))
+    fin = np.isfinite(ref)
+    assert np.array_equal(fin, np.isfinite(out))
+    rel = np.abs(out[fin] - ref[fin]) / np.maximum(np.abs(ref[fin]), 1e-300)
+    assert rel.max(initial=0) <= rtol
+
+
+@pytest.mark.parametrize("scene", list(EST_SCENES))
+@pytest.mark.parametrize("est", [2, 3, 4])
+def test_per_sample_vs_reference_e234(samples_e234, orc, scene, est):
+    orc.set_scene(samples_e234[f"{scene}__scene"])
+    k = f"{scene}__e{est}__"
+    L, st = orc.trace(est, samples_e234[k + "ray"], samples_e234[k + "state1"])
+    assert np.array_equal(st, samples_e234[k + "state2"]), "random draws consumed differ"
+    _close_nan_aware(L, samples_e234[k + "L"])
+
+
+@pytest.mark.parametrize("scene", list(EST_SCENES))
+@pytest.mark.parametrize("est", [2, 3, 4])
+def test_framebuffer_vs_reference_e234(samples_e234, orc, scene, est):
+    orc.set_scene(samples_e234[f"{scene}__scene"])
+    out = orc.render(24, 24, 4, est, seed=SEED, threads=2, chunk=4)  # chunk = spp: the reference's order
+    _close_nan_aware(out, samples_e234[f"{scene}__e{est}__fb24x24x4"])
+
+
+def test_explicit_free_is_the_free_flight_loop(samples_e234, orc):
+    """the recursive FF twin equals iterativeVPTracerFree up to reassociation -- same
+    draws, same branches, values within 1e-12."""
+    orc.set_scene(samples_e234["default__scene"])
+    k = "default__e2__"
+    L0, s0 = orc.trace(0, samples_e234[k + "ray"], samples_e234[k + "state1"])
+    assert np.array_equal(s0, samples_e234[k + "state2"])
+    _close_nan_aware(L0, samples_e234[k + "L"])
