@@ -44,6 +44,12 @@ def samples_e234():
 
 
 @pytest.fixture(scope="session")
+def samples_alt():
+    """the reference's alternate scenes x all five estimators (make_golden.py --alt-scenes)"""
+    return dict(np.load(os.path.join(GOLDEN, "samples_alt.npz")))
+
+
+@pytest.fixture(scope="session")
 def prims():
     return dict(np.load(os.path.join(GOLDEN, "primitives.npz")))
 

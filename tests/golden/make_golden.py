@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(HERE))
 
 from oracle.oracle import Reference  # noqa: E402
-from scenes import EST_SCENES, SCENES, stream_state  # noqa: E402
+from scenes import ALT_SCENES, EST_SCENES, SCENES, stream_state  # noqa: E402
 
 SEED = 0x5EED0001
 W = H = 64
@@ -238,9 +238,31 @@ def estimators_234():
     print("wrote", os.path.join(HERE, "samples_e234.npz"))
 
 
+def alt_scenes():
+    """The reference's alternate scenes (commented out in include/Sphere.cpp:27-105, restated in
+    tests/scenes.py ALT_SCENES) through all five estimators -> samples_alt.npz."""
+    ref = Reference()
+    rng = np.random.default_rng(20261016)
+    bundle = {}
+    for name, mk in ALT_SCENES.items():
+        sc = mk()
+        ref.set_scene(sc)
+        bundle[f"{name}__scene"] = sc.view(np.uint8)
+        for est in range(5):
+            ps = per_sample(ref, est, 256, rng)
+            for k, v in ps.items():
+                bundle[f"{name}__e{est}__{k}"] = v
+            bundle[f"{name}__e{est}__fb24x24x4"] = ref.render(24, 24, 4, est, seed=SEED)
+    np.savez_compressed(os.path.join(HERE, "samples_alt.npz"), **bundle)
+    print("wrote", os.path.join(HERE, "samples_alt.npz"))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["--estimators-234"]:
         estimators_234()
+    elif sys.argv[1:] == ["--alt-scenes"]:
+        alt_scenes()
     else:
         main()
         estimators_234()
+        alt_scenes()

@@ -91,6 +91,76 @@ SCENES = {
 # scenes of the estimator fixtures (tests/golden/samples_e234.npz)
 EST_SCENES = dict(SCENES, big_light=big_light_scene)
 
+# ---- the reference's alternate scenes (commented out in include/Sphere.cpp), as parity cases
+AL2_ETA, AL2_KAPPA = (0.143245, 0.377423, 1.43919), (3.98479, 2.3847, 1.60434)
+
+
+def alt_metal_walls_scene():
+    """include/Sphere.cpp:27-45 ("escena dos"): conductor side walls, coloured box, one point light."""
+    return np.concatenate([
+        sph(1e5, (-1e5 - 49, 0, 0), mat=1, eta=AL_ETA, kappa=AL_KAPPA, alpha=0.03),
+        sph(1e5, (1e5 + 49, 0, 0), mat=1, eta=AL_ETA, kappa=AL_KAPPA, alpha=0.03),
+        sph(1e5, (0, 0, -1e5 - 81.6), (.25, .75, .25)),
+        sph(1e5, (0, -1e5 - 40.8, 0), (.25, .75, .75)),
+        sph(1e5, (0, 1e5 + 40.8, 0), (.75, .75, .25)),
+        sph(16.5, (-23, -24.3, -34.6), (.75, .75, .25)),
+        sph(16.5, (23, -24.3, -3.6), (.4, .3, .2)),
+        sph(0, (14, -24.3, -35), rad=(2000, 2000, 3000)),
+    ])
+
+
+def alt_light_near_camera_scene():
+    """include/Sphere.cpp:47-60 ("escena 3"): no walls, two spheres and a point light right in
+    front of the camera."""
+    return np.concatenate([
+        sph(30, (0, 11.2, 165), (.0, .25, .75)),
+        sph(16.5, (0, -10, 200), (.75, .75, .75)),
+        sph(0, (0, 11.2, 204), rad=(400, 400, 400)),
+    ])
+
+
+def alt_area_light_scene():
+    """include/Sphere.cpp:62-74: coloured box without ceiling, conductor sphere, one r=12 area light."""
+    return np.concatenate([
+        sph(1e5, (-1e5 - 49, 0, 0), (.75, .25, .25)),
+        sph(1e5, (1e5 + 49, 0, 0), (.25, .25, .75)),
+        sph(1e5, (0, 0, -1e5 - 81.6), (.25, .75, .25)),
+        sph(1e5, (0, -1e5 - 40.8, 0), (.25, .75, .75)),
+        sph(16.5, (-23, -24.3, -34.6), mat=1, eta=AL_ETA, kappa=AL_KAPPA, alpha=0.03),
+        sph(12, (24, 24.3, -50), rad=(0, 800, 800)),
+    ])
+
+
+def alt_open_space_scene():
+    """include/Sphere.cpp:76-86 ("primitive infinite"): no walls, conductor spheres floating in the
+    medium, three point lights -- rays escape (t = MAXFLOAT paths)."""
+    return np.concatenate([
+        sph(16.5, (-23, -24.3, -34.6), mat=1, eta=AL_ETA, kappa=AL_KAPPA, alpha=0.03),
+        sph(16.5, (23, -24.3, -3.6), mat=1, eta=AL2_ETA, kappa=AL2_KAPPA, alpha=0.3),
+        sph(100, (0, -24.3, -200), mat=1, eta=AL2_ETA, kappa=AL2_KAPPA, alpha=0.02),
+        sph(0, (24, 24.3, -3.6), rad=(2000, 2000, 2000)),
+        sph(0, (-24, 10, -34.6), rad=(2000, 5000, 1000)),
+        sph(0, (0, -24.3, -30), rad=(4000, 8000, 4000)),
+    ])
+
+
+def alt_point_box_scene():
+    """include/Sphere.cpp:88-105: grey box, one Lambert sphere, two point lights."""
+    return np.concatenate(walls((.5, .5, .5), (.5, .5, .5)) + [
+        sph(16.5, (23, -24.3, -3.6), (.50, .50, 0)),
+        sph(0, (-23, 0, -10.6), (1, 1, 1), rad=(6000, 6000, 6000)),
+        sph(0, (23, 24.3, -50), (1, 1, 1), rad=(4000, 4000, 4000)),
+    ])
+
+
+ALT_SCENES = {
+    "alt_metal_walls": alt_metal_walls_scene,
+    "alt_light_near_camera": alt_light_near_camera_scene,
+    "alt_area_light": alt_area_light_scene,
+    "alt_open_space": alt_open_space_scene,
+    "alt_point_box": alt_point_box_scene,
+}
+
 
 # independent (pure Python) statement of the per-sample stream spec (csrc/vpt_rng.h)
 M64 = (1 << 64) - 1

@@ -312,3 +312,24 @@ def test_count_work_matches_oracle_e234(gpu_tracer, orc_vm):
         t, it = gpu_tracer.count_work(vpt.RenderConfig(width=32, height=24, spp=4, estimator=est, seed=9))
         _, c = orc_vm.render(32, 24, 4, est, seed=9, counters=True)
         assert (t, it) == (c.tests, c.iterations)
+
+
+# ---------------------------------------------------------------- alternate scenes x 5 estimators
+from scenes import ALT_SCENES  # noqa: E402
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", list(ALT_SCENES))
+@pytest.mark.parametrize("est", [0, 1, 2, 3, 4])
+def test_alt_scenes_vs_oracle_bitwise(gpu_tracer, orc_vm, samples_alt, scene, est):
+    sc = samples_alt[f"{scene}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    k = f"{scene}__e{est}__"
+    rays, st = samples_alt[k + "ray"], samples_alt[k + "state1"]
+    L, s = gpu_tracer.trace(est, _rays(rays), st)
+    Lo, so = orc_vm.trace(est, rays, st)
+    assert np.array_equal(s, so)
+    assert bitwise_equal(L, Lo).all()
+    g = gpu_tracer.render(width=24, height=20, spp=6, estimator=est, seed=SEED, fp64=True)
+    assert bitwise_equal(g, orc_vm.render(24, 20, 6, est, seed=SEED)).all()

@@ -229,3 +229,25 @@ def test_explicit_free_is_the_free_flight_loop(samples_e234, orc):
     L0, s0 = orc.trace(0, samples_e234[k + "ray"], samples_e234[k + "state1"])
     assert np.array_equal(s0, samples_e234[k + "state2"])
     _close_nan_aware(L0, samples_e234[k + "L"])
+
+
+# ---- the reference's alternate scenes (include/Sphere.cpp:27-105) through all five estimators
+from scenes import ALT_SCENES  # noqa: E402
+
+
+@pytest.mark.parametrize("scene", list(ALT_SCENES))
+@pytest.mark.parametrize("est", [0, 1, 2, 3, 4])
+def test_alt_scenes_vs_reference(samples_alt, orc, scene, est):
+    orc.set_scene(samples_alt[f"{scene}__scene"])
+    k = f"{scene}__e{est}__"
+    L, st = orc.trace(est, samples_alt[k + "ray"], samples_alt[k + "state1"])
+    assert np.array_equal(st, samples_alt[k + "state2"]), "random draws consumed differ"
+    if est == 0:
+        assert bitwise_equal(L, samples_alt[k + "L"]).all()
+    else:
+        _close_nan_aware(L, samples_alt[k + "L"])
+    out = orc.render(24, 24, 4, est, seed=SEED, threads=2, chunk=4)
+    if est == 0:
+        assert bitwise_equal(out, samples_alt[k + "fb24x24x4"]).all()
+    else:
+        _close_nan_aware(out, samples_alt[k + "fb24x24x4"])
