@@ -199,7 +199,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                                        const Medium& m, Sampler<COUNT>& smp, Task& t, bool active, int lane,
                                        uint64_t below, bool dbg, ADbg& D)
 {
-    bool done = !active, parked = false;
+    bool done = !active, parked = false, fresh = false;
     if (active && t.killed) {  /* the S/M roulette ended the path */
         t.acc = add(t.p.L, t.acc);  /* src/rt.cpp:794 */
         t.in_path = false;
@@ -260,23 +260,33 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             } else {
                 const int x = (int)(t.pix & 0xFFFFu), y = (int)(t.pix >> 16);
                 const uint64_t idx = (uint64_t)(P.h - 1 - y) * (uint64_t)P.w + (uint64_t)x;  /* src/rt.cpp:773 */
-                smp.X = vpt_stream_start(P.seed, idx, (uint64_t)t.i);
+                const uint64_t X0 = vpt_stream_start(P.seed, idx, (uint64_t)t.i);
                 ++t.i;
                 if (dbg) ++D.samples;
-                const double jx = smp.next();  /* src/rt.cpp:787, x draw first */
-                const double jy = smp.next();
-                t.p.depth = 0;
-                if (continue_path(smp, t.p, m)) {
-                    t.p.o = mk(P.o[0], P.o[1], P.o[2]);
-                    t.p.d = pool_camera_dir(P, jx, jy, x, y);
-                    t.p.beta = mk(1, 1, 1);
-                    t.p.L = mk(0, 0, 0);
+                /* the first roulette draw (vptShadeMethods.h:1282, continue_path at depth 0) is the
+                 * stream's third, after the jitter pair: decide it from the state three steps on;
+                 * the jitter and the camera ray are built after the loop, for survivors only */
+                if (COUNT) smp.cnt.iterations++;
+                if (!(vpt_erand48_value(vpt_erand48_skip3(X0)) < 1 - 0.6)) {
+                    t.X = X0;
                     t.in_path = true;
-                    t.X = smp.X;
+                    fresh = true;
                 }
             }
         }
         if (__ballot(!done && !parked && !t.in_path) == 0) break;
+    }
+    if (fresh) {  /* camera ray of the surviving sample: src/rt.cpp:787-789 */
+        smp.X = t.X;
+        const double jx = smp.next();  /* x draw first */
+        const double jy = smp.next();
+        (void)smp.next();  /* the roulette draw, decided above */
+        t.p.o = mk(P.o[0], P.o[1], P.o[2]);
+        t.p.d = pool_camera_dir(P, jx, jy, (int)(t.pix & 0xFFFFu), (int)(t.pix >> 16));
+        t.p.beta = mk(1, 1, 1);
+        t.p.L = mk(0, 0, 0);
+        t.p.depth = 0;
+        t.X = smp.X;
     }
     const unsigned long long c1 = dbg_clock(dbg);
     int result = parked ? R_A : R_DONE;

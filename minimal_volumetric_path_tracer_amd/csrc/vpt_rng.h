@@ -38,17 +38,30 @@ VPT_HD uint64_t vpt_stream_start(uint64_t seed, uint64_t idx, uint64_t sample)
     return vpt_splitmix64(k ^ (sample * 0xD1B54A32D192ED03ull + 1ull)) >> 16;
 }
 
-/* one erand48 draw: advances X, returns X/2^48 exactly (glibc erand48_r construction) */
-VPT_HD double vpt_erand48(uint64_t* X)
+/* the value erand48 returns when its state has become x: x/2^48 exactly (glibc erand48_r
+ * construction: the mantissa of 1.m from x<<4, minus 1.0) */
+VPT_HD double vpt_erand48_value(uint64_t x)
 {
-    uint64_t x = (*X * 0x5DEECE66Dull + 0xBull) & 0xFFFFFFFFFFFFull;
-    *X = x;
     union {
         uint64_t u;
         double d;
     } b;
     b.u = 0x3FF0000000000000ull | (x << 4);
     return b.d - 1.0;
+}
+
+/* one erand48 draw: advances X, returns X/2^48 exactly */
+VPT_HD double vpt_erand48(uint64_t* X)
+{
+    uint64_t x = (*X * 0x5DEECE66Dull + 0xBull) & 0xFFFFFFFFFFFFull;
+    *X = x;
+    return vpt_erand48_value(x);
+}
+
+/* the state three draws later, in one step: a^3 X + c (a^2 + a + 1) mod 2^48 */
+VPT_HD uint64_t vpt_erand48_skip3(uint64_t X)
+{
+    return (X * 0xD498BD0AC4B5ull + 0xAA8544E593Dull) & 0xFFFFFFFFFFFFull;
 }
 
 #endif
