@@ -46,7 +46,9 @@ struct ADbg {
 };
 __device__ __forceinline__ unsigned long long dbg_clock(bool dbg) { return dbg ? __builtin_amdgcn_s_memtime() : 0; }
 
-enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_BX, F_BY, F_BZ, F_LX, F_LY, F_LZ, F_AX, F_AY, F_AZ, F_T, F_DIST,
+/* F_TD: the pending event's distance -- surface t for stage S, sampled distance for stage M (each
+ * stage reads only its own); F_KEY: the unit's pixel stream key (vpt_stream_key), as raw bits */
+enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_BX, F_BY, F_BZ, F_LX, F_LY, F_LZ, F_AX, F_AY, F_AZ, F_TD, F_KEY,
        F_PDF };
 
 struct TaskPool {
@@ -120,6 +122,7 @@ struct Task {
     Event e;
     dv3 acc;
     uint64_t X;
+    uint64_t key;    /* the unit's pixel stream key */
     unsigned pix;    /* x | camera row << 16 */
     unsigned c1;     /* one past the unit's last sample; 0 = the task needs a unit */
     unsigned i;      /* next sample to start */
@@ -132,8 +135,7 @@ __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bo
     t.p.d = mk(sh.f[F_DX][s], sh.f[F_DY][s], sh.f[F_DZ][s]);
     t.p.beta = mk(sh.f[F_BX][s], sh.f[F_BY][s], sh.f[F_BZ][s]);
     t.p.L = mk(sh.f[F_LX][s], sh.f[F_LY][s], sh.f[F_LZ][s]);
-    t.e.t = sh.f[F_T][s];
-    t.e.dist = sh.f[F_DIST][s];
+    t.e.t = t.e.dist = sh.f[F_TD][s];
     t.e.pdf = sh.f[F_PDF][s];
     const uint32_t ev = sh.evw[s];
     t.p.depth = (int)(ev & 0xFFFFu);
@@ -143,6 +145,7 @@ __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bo
     t.X = sh.X[s];
     if (full) {
         t.acc = mk(sh.f[F_AX][s], sh.f[F_AY][s], sh.f[F_AZ][s]);
+        t.key = (uint64_t)__double_as_longlong(sh.f[F_KEY][s]);
         t.pix = sh.pix[s];
         t.c1 = sh.c1[s];
         const uint32_t sm = sh.samp[s];
@@ -161,8 +164,8 @@ __device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, b
     sh.evw[s] = (uint32_t)(t.p.depth & 0xFFFF) | ((uint32_t)t.e.id << 16) | ((uint32_t)t.e.src << 24) |
                 (t.killed ? 0x80000000u : 0u);
     if (full) {
-        sh.f[F_T][s] = t.e.t;
-        sh.f[F_DIST][s] = t.e.dist;
+        sh.f[F_TD][s] = t.e.t;  /* stage_a leaves the distance the next stage reads in e.t */
+        sh.f[F_KEY][s] = __longlong_as_double((long long)t.key);
         sh.f[F_PDF][s] = t.e.pdf;
         sh.f[F_AX][s] = t.acc.x; sh.f[F_AY][s] = t.acc.y; sh.f[F_AZ][s] = t.acc.z;
         sh.pix[s] = t.pix;
@@ -245,6 +248,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                     const Unit uu = decode_unit(P, sh.uring[(h + r) % URING]);
                     if (uu.valid) {  /* (an invalid unit -- a tile's padding -- is dropped) */
                         t.pix = (unsigned)uu.x | ((unsigned)uu.y << 16);
+                        t.key = vpt_stream_key(P.seed, (uint64_t)(P.h - 1 - uu.y) * (uint64_t)P.w + (uint64_t)uu.x);
                         t.i = (unsigned)(uu.c * P.chunk);
                         t.c1 = (unsigned)min((uu.c + 1) * P.chunk, P.spp);
                         t.in_path = false;
@@ -258,9 +262,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                 store_partial(P, t);
                 t.c1 = 0;
             } else {
-                const int x = (int)(t.pix & 0xFFFFu), y = (int)(t.pix >> 16);
-                const uint64_t idx = (uint64_t)(P.h - 1 - y) * (uint64_t)P.w + (uint64_t)x;  /* src/rt.cpp:773 */
-                const uint64_t X0 = vpt_stream_start(P.seed, idx, (uint64_t)t.i);
+                const uint64_t X0 = vpt_stream_start_key(t.key, (uint64_t)t.i);  /* key: src/rt.cpp:773 idx */
                 ++t.i;
                 if (dbg) ++D.samples;
                 /* the first roulette draw (vptShadeMethods.h:1282, continue_path at depth 0) is the
@@ -303,6 +305,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             result = R_S + (sk == 0 ? (EST == 3 ? 0 : S->geo[t.e.src].point) : sk);
         } else {
             result = R_M + (EST == 3 ? 0 : S->geo[t.e.src].point);
+            t.e.t = t.e.dist;  /* one slot (F_TD): stage M reads the sampled distance */
         }
     }
     if (dbg) {

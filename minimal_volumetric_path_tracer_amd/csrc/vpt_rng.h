@@ -31,11 +31,22 @@ VPT_HD uint64_t vpt_splitmix64(uint64_t z)
     return z ^ (z >> 31);
 }
 
-/* start state of sample `sample` of the pixel with file-order index `idx` (src/rt.cpp:773) */
+/* the pixel's key: file-order index `idx` (src/rt.cpp:773) under the image seed */
+VPT_HD uint64_t vpt_stream_key(uint64_t seed, uint64_t idx)
+{
+    return vpt_splitmix64(seed + 0x9E3779B97F4A7C15ull * (idx + 1ull));
+}
+
+/* start state of sample `sample` of the pixel with key `key` */
+VPT_HD uint64_t vpt_stream_start_key(uint64_t key, uint64_t sample)
+{
+    return vpt_splitmix64(key ^ (sample * 0xD1B54A32D192ED03ull + 1ull)) >> 16;
+}
+
+/* start state of sample `sample` of the pixel with file-order index `idx` */
 VPT_HD uint64_t vpt_stream_start(uint64_t seed, uint64_t idx, uint64_t sample)
 {
-    uint64_t k = vpt_splitmix64(seed + 0x9E3779B97F4A7C15ull * (idx + 1ull));
-    return vpt_splitmix64(k ^ (sample * 0xD1B54A32D192ED03ull + 1ull)) >> 16;
+    return vpt_stream_start_key(vpt_stream_key(seed, idx), sample);
 }
 
 /* the value erand48 returns when its state has become x: x/2^48 exactly (glibc erand48_r
