@@ -122,6 +122,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="ff", choices=list(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--chunk", type=int, default=0, help="samples per work unit (0 = auto, min(spp, 32))")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -144,7 +145,8 @@ def main() -> None:
     band = BAND_ROWS if world > 1 else H
     if world > 1 and H % (band * world):
         raise SystemExit("image height must be a multiple of 16 * world size")
-    cfg = vpt.RenderConfig(**c, seed=0x5EED0001, band_rows=band, band_stride=world, band_offset=rank)
+    cfg = vpt.RenderConfig(**c, seed=0x5EED0001, band_rows=band, band_stride=world, band_offset=rank,
+                           chunk_spp=args.chunk)
     tracer = vpt.Tracer(dev.index)
     rows = cfg.shard_rows()
     out = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)

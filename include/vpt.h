@@ -98,7 +98,7 @@ typedef struct vpt_params {
      * and writes them compactly, in increasing file-row order.  Whole image: band_rows = height,
      * band_stride = 1, band_offset = 0 (vpt_default_params). */
     int32_t band_rows, band_stride, band_offset;
-    /* Samples per partial sum (build extension; 0 = auto = ceil(spp/16)).  A pixel's samples are
+    /* Samples per partial sum (build extension; 0 = auto = min(spp, 32)).  A pixel's samples are
      * summed sequentially inside a chunk exactly as the reference sums a pixel (src/rt.cpp:794),
      * and the chunk sums are then added in chunk order; chunk_spp == 1 or >= spp is the
      * reference's own sequential order.  Chunks are the GPU's unit of work. */

@@ -68,7 +68,7 @@ def _bind(L: ctypes.CDLL, prefix: str) -> ctypes.CDLL:
 
 def default_chunk(spp: int) -> int:
     """samples per chunk the GPU uses when vpt_params.chunk_spp == 0 (csrc/vpt_kernels.hip)"""
-    return max(1, (spp + 15) // 16)
+    return min(spp, 32)
 
 
 class Oracle:
@@ -119,7 +119,7 @@ class Oracle:
     def render(self, w, h, spp, estimator=0, sigma_a=0.001, sigma_s=0.009, hg_g=0.0, max_depth=0, seed=0x5EED0001,
                y0=0, y1=None, threads=0, counters=False, chunk=None):
         """main()'s pixel loop over camera rows [y0, y1); returns (h, w, 3) float64 in file order.
-        chunk: samples per partial sum (None = the GPU's default, ceil(spp/16); spp = reference order)."""
+        chunk: samples per partial sum (None = the GPU's default, min(spp, 32); spp = reference order)."""
         m = Medium(sigma_a, sigma_s, hg_g, max_depth, estimator)
         out = np.zeros((h, w, 3))
         c = Counters()

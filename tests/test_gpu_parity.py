@@ -110,14 +110,14 @@ def test_render_vs_oracle_bitwise(gpu_tracer, orc_vm, est):
     assert bitwise_equal(g32, o.astype(np.float32)).all()
 
 
-@pytest.mark.parametrize("spp,chunk", [(40, 0), (40, 7), (40, 40), (40, 1), (33, 0)])
+@pytest.mark.parametrize("spp,chunk", [(40, 0), (40, 7), (40, 40), (40, 1), (33, 0), (70, 0)])
 def test_chunked_sums_vs_oracle(gpu_tracer, orc_vm, spp, chunk):
-    """spp > 16: samples summed in chunks (vpt_params.chunk_spp); chunk 1 or spp = reference order."""
+    """samples summed in chunks (vpt_params.chunk_spp; auto = min(spp, 32)); chunk 1 or spp = reference order."""
     sc = SCENES["default"]()
     gpu_tracer.set_scene(sc)
     orc_vm.set_scene(sc)
     g = gpu_tracer.render(width=20, height=12, spp=spp, chunk_spp=chunk, seed=4, fp64=True)
-    eff = chunk if chunk > 0 else (spp + 15) // 16
+    eff = chunk if chunk > 0 else min(spp, 32)
     o = orc_vm.render(20, 12, spp, 0, seed=4, chunk=eff, threads=4)
     assert bitwise_equal(g, o).all()
     if chunk in (1, spp):
