@@ -32,6 +32,12 @@
 #ifndef VPT_ISECT_UNROLL
 #define VPT_ISECT_UNROLL 5
 #endif
+/* rays from the surface point intersected in one pass by MISv2 (0 = off, 2, 3): bit-exact, but
+ * measured slower in the pool kernel (off / 2 / 3: 4148 / 4036 / 4063 Ms/s) -- the extra live
+ * registers spill at 256 VGPRs; kept for a kernel with a separate surface-stage register budget */
+#ifndef VPT_FUSE_RAYS
+#define VPT_FUSE_RAYS 0
+#endif
 
 namespace vpt {
 
@@ -528,6 +534,186 @@ VPT_DEV dv3 mis_v2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj,
     return add(mc, scl(g, wg));
 }
 
+/* intersect() (include/pathTracingUtilities.h:12-36) of N rays from ONE origin in one pass over the
+ * spheres: per ray exactly the operations of scene_intersect, in the same order (oc and |oc|^2 are
+ * the same numbers for every ray, so they are formed once), and N independent dependency chains
+ * per sphere instead of one.  id[k] must be initialised by the caller (left unchanged on a miss,
+ * like scene_intersect). */
+template <int N, bool COUNT>
+VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, const dv3 (&d)[N],
+                               double (&t)[N], int (&id)[N], bool (&hit)[N])
+{
+    double tmin[N];
+    bool contact[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        tmin[k] = VPT_DBL_MAX;
+        contact[k] = false;
+    }
+    const int n = S->n;
+    for (int i = 0; i < n; ++i) {
+        const GeoSphere g = S->geo[i];
+        const double ocx = o.x - g.px, ocy = o.y - g.py, ocz = o.z - g.pz;
+        const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const double b = ocx * d[k].x + ocy * d[k].y + ocz * d[k].z;
+            const double det = b * b - cc + g.r2;
+            double tact = 0.0;
+            if (det >= 0) {
+                const double sq = vm_sqrt(det);
+                const double t2 = -b + sq;
+                const double t1 = -b - sq;
+                tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
+            }
+            if (tact > 0 && vm_fabs(tact) > 0.0001) {
+                contact[k] = true;
+                if (tact < tmin[k]) {
+                    tmin[k] = tact;
+                    id[k] = i;
+                }
+            }
+        }
+    }
+    smp.tests(N * n);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        hit[k] = contact[k];
+        t[k] = contact[k] ? tmin[k] : 0.0;
+    }
+}
+
+/* MISv2 (include/misSamplingFunctions.h:96-170) for a scene with exactly two MIS lights, same bits
+ * and draws as mis_v2: every draw of MISv2 precedes, and none depends on, the three ray casts
+ * (the two light samples of muestreoSA, :163-206, and the BSDF sample of uniform / softDielectric
+ * / microfacet), so the draws and directions are taken first in the reference's order, the three
+ * rays from x are intersected in one pass (scene_intersect_n), and the arithmetic is then done in
+ * the reference's order. */
+template <bool COUNT>
+VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray,
+                              double alpha, double sigma_t)
+{
+    const int omat = S->sph[obj].material;
+    const dv3 wo = scl(wray, -1);
+    /* ---- draws and directions, in the reference's order */
+    int lt[2];
+    dv3 dirs[3];
+    double cm[2], xtra[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        lt[k] = S->mis_light[k];
+        dv3 cx = sub(sph_p(S, lt[k]), x);
+        const double normcx = vm_sqrt(dot(cx, cx));
+        cx = scl(cx, (1 / normcx));
+        const double lr = S->sph[lt[k]].r;
+        cm[k] = vm_sqrt(1 - (lr / normcx) * (lr / normcx));
+        dirs[k] = solid_angle_dir(smp, cx, cm[k]);
+        if (omat == 2) xtra[k] = smp.next();  /* the dielectric pdf coin of the light loop */
+    }
+    dv3 wt_s = mk(0, 0, 0), wh_m = mk(0, 0, 0), wo_l = mk(0, 0, 0), wi_m = mk(0, 0, 0);
+    bool refl = false;
+    if (omat == 0) {
+        dirs[2] = nrm(cosine_hemispheric(smp, n));  /* uniform(), samplingFunctions.h:250-261 */
+    } else if (omat == 2) {  /* softDielectric, samplingFunctions.h:209-235 */
+        wt_s = nrm(refrax_dielectric(1.0, 1.5, wo, n));
+        const double F = fresnel_die(1.0, 1.5, dot(n, wt_s), dot(n, wo));
+        refl = smp.next() < F;
+        dirs[2] = refl ? nrm(reflex_dielectric(wo, n)) : wt_s;
+    } else {  /* vectorFacet + microfacet, samplingFunctions.h:97-118 */
+        wh_m = vector_facet(smp, alpha);
+        wo_l = nrm(to_local(n, wo));
+        wi_m = nrm(add(scl(wo_l, -1), scl(scl(wh_m, 2), dot(wh_m, wo_l))));
+        dirs[2] = nrm(from_local(n, wi_m.x, wi_m.y, wi_m.z));
+    }
+    /* ---- the three ray casts from x */
+    double tt[3];
+    int ids[3] = {0, 0, 0};
+    bool hits[3];
+#if VPT_FUSE_RAYS == 3
+    scene_intersect_n<3>(S, smp, x, dirs, tt, ids, hits);
+#else
+    {
+        const dv3 d2[2] = {dirs[0], dirs[1]};
+        double t2[2];
+        int i2[2] = {0, 0};
+        bool h2[2];
+        scene_intersect_n<2>(S, smp, x, d2, t2, i2, h2);
+        ids[0] = i2[0];
+        ids[1] = i2[1];
+        hits[2] = scene_intersect(S, smp, x, dirs[2], tt[2], ids[2], false);
+    }
+#endif
+    /* ---- the reference's arithmetic */
+    dv3 mc = mk(0, 0, 0);
+    double fpdf = 0, gpdf = 0, cmax = 0, wg;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const dv3 wi = dirs[k];
+        const dv3 wilocal = nrm(to_local(n, wi));
+        const dv3 wolocal = nrm(to_local(n, wo));
+        const dv3 wh = nrm(add(wilocal, wolocal));
+        dv3 fr;
+        if (omat == 0) fr = scl(sph_c(S, obj), (1 / VPT_PI));
+        else if (omat == 2) fr = mk(0, 0, 0);
+        else fr = fr_microfacet(ld3(S->sph[obj].eta), ld3(S->sph[obj].kappa), wilocal, wh, wolocal, alpha, mk(0, 0, 1));
+        const dv3 Le = (lt[k] == ids[k]) ? sph_rad(S, ids[k]) : mk(0, 0, 0);
+        dv3 f = scl(scl(mul(Le, fr), dot(n, wi)), (1 / solid_angle_prob(cm[k])));
+        f = scl(f, transmitance(x, sph_p(S, lt[k]), sigma_t));
+        cmax = cm[k];
+        fpdf = solid_angle_prob(cmax);
+        if (omat == 0) {
+            gpdf = hemi_cosine_prob(dot(n, wi));
+        } else if (omat == 2) {
+            const dv3 wt = nrm(refrax_dielectric(1.0, 1.5, wo, n));
+            gpdf = fresnel_die(1.0, 1.5, dot(n, wt), dot(n, wo));
+            if (xtra[k] > gpdf) gpdf = 1 - gpdf;
+        } else {
+            const dv3 whg = nrm(add(wi, wo));
+            gpdf = microfacet_prob(wo, whg, alpha, n);
+        }
+        const double wf = power_heuristic(fpdf, gpdf);
+        mc = add(mc, scl(f, wf));
+    }
+    dv3 g;
+    const dv3 Lb = hits[2] ? sph_rad(S, ids[2]) : mk(0, 0, 0);  /* rayTracer */
+    const int sourceid = hits[2] ? ids[2] : 0;
+    if (omat == 0) {
+        const dv3 wi = dirs[2];
+        g = add(mk(0, 0, 0), scl(scl(mul(Lb, scl(sph_c(S, obj), (1 / VPT_PI))), dot(n, wi)), (1 / hemi_cosine_prob(dot(n, wi)))));
+        gpdf = hemi_cosine_prob(dot(n, wi));
+        if (g.x > 0 && g.y > 0 && g.z > 0) {
+            cmax = cos_theta_max(S, sourceid, x);
+            fpdf = solid_angle_prob(cmax);
+            wg = power_heuristic(gpdf, fpdf);
+        } else {
+            wg = 0;
+        }
+    } else if (omat == 2) {
+        if (refl) {
+            g = scl(Lb, (1 / vm_fabs(dot(n, dirs[2]))));
+        } else {
+            const double ratio = 1.5 / 1.0;
+            g = scl(scl(scl(Lb, (1 / vm_fabs(dot(n, wt_s)))), ratio), ratio);
+        }
+        if (g.x > 0 && g.y > 0 && g.z > 0) {
+            cmax = cos_theta_max(S, sourceid, x);
+            fpdf = solid_angle_prob(cmax);
+            wg = power_heuristic(gpdf, fpdf); /* gpdf: stale value from the light loop (reference) */
+        } else {
+            wg = 0;
+        }
+    } else {
+        const dv3 nl = mk(0, 0, 1);
+        const dv3 fr = fr_microfacet(ld3(S->sph[obj].eta), ld3(S->sph[obj].kappa), wi_m, wh_m, wo_l, alpha, nl);
+        g = scl(scl(mul(Lb, fr), dot(mk(0, 0, 1), wi_m)), (1 / microfacet_prob(wo_l, wh_m, alpha, nl)));
+        gpdf = microfacet_prob(wo_l, wh_m, alpha, mk(0, 0, 1));
+        if (g.x > 0) cmax = cos_theta_max(S, sourceid, x);
+        fpdf = solid_angle_prob(cmax);
+        wg = power_heuristic(gpdf, fpdf);
+    }
+    return add(mc, scl(g, wg));
+}
+
 /* bdsf (continuation sample), include/vptShadeMethods.h:16-59 */
 template <bool COUNT>
 VPT_DEV dv3 bdsf(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3& aux, dv3 wray, dv3 n, double& prob, int id)
@@ -784,7 +970,12 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     const double alpha = S->sph[id].alpha;
     double Trs = transmitance(xs, sph_p(S, src), sigma_t);
     dv3 Ldp = scl(scl(p_light(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+#if VPT_FUSE_RAYS
+    dv3 Ld = S->n_mis == 2 ? mis_v2_two_lights(S, smp, id, xs, nx, p.d, alpha, sigma_t)
+                           : mis_v2(S, smp, id, xs, nx, p.d, alpha, sigma_t);
+#else
     dv3 Ld = mis_v2(S, smp, id, xs, nx, p.d, alpha, sigma_t);
+#endif
     dv3 wi = mk(0, 0, 0);
     double pdf = 0;
     dv3 fs = bdsf(S, smp, wi, p.d, nx, pdf, id);
