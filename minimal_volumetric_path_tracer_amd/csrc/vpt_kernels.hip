@@ -389,6 +389,8 @@ static int env_int(const char* name, int dflt)
 
 template <int EST, bool COUNT, int FB>
 static int launch_wave(vpt_context* ctx, KParams K, hipStream_t stream);
+template <int EST, int FB>
+static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream);
 
 template <int EST, bool COUNT, int FB>
 static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
@@ -402,6 +404,15 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         HIP_OK(hipGetLastError());
         return VPT_OK;
     }
+    if constexpr (!COUNT) return launch_pool<EST, FB>(ctx, K, stream);
+    return VPT_OK;
+}
+
+template <int EST, int FB>
+static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
+{
+    const DevScene* S = ctx->d_scene;
+    constexpr bool COUNT = false;
     int blocks = 0;
     int rc;
     const bool wave = EST <= 1 && env_int("VPT_WAVE_KERNEL", 0);  /* A/B: the previous design, FF/MIS */
