@@ -201,10 +201,12 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
 }
 
 /* ------------------------------------------------------------------ sampling */
-VPT_DEV dv3 dir_from_angles(dv3 n, double theta, double phi)
+/* direction at polar angle theta = acos(c) and azimuth phi around n; sin/cos of the acos as the
+ * build's libm evaluates them (vm_sincos_acos) */
+VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
 {
     double st, ct, sp, cp;
-    vm_sincos(theta, &st, &ct);
+    vm_sincos_acos(c, &st, &ct);
     vm_sincos(phi, &sp, &cp);
     return nrm(from_local(n, st * cp, st * sp, ct));
 }
@@ -214,9 +216,9 @@ template <bool COUNT>
 VPT_DEV dv3 solid_angle_dir(Sampler<COUNT>& smp, dv3 wc, double cmax)
 {
     double e0 = smp.next();
-    double theta = vm_acos((1 - e0) + e0 * cmax);
+    double c = (1 - e0) + e0 * cmax;  /* theta = acos(c) */
     double phi = 2 * VPT_PI * smp.next();
-    return dir_from_angles(wc, theta, phi);
+    return dir_from_cos(wc, c, phi);
 }
 
 /* solidAngleProb, include/samplingFunctions.h:85-87 */
@@ -228,9 +230,9 @@ VPT_DEV double hemi_cosine_prob(double c) { return c * 1 / VPT_PI; }
 template <bool COUNT>
 VPT_DEV dv3 cosine_hemispheric(Sampler<COUNT>& smp, dv3 n)
 {
-    double theta = vm_acos(vm_sqrt(1 - smp.next()));
+    double c = vm_sqrt(1 - smp.next());  /* theta = acos(c) */
     double phi = 2 * VPT_PI * smp.next();
-    return dir_from_angles(n, theta, phi);
+    return dir_from_cos(n, c, phi);
 }
 
 /* isotropicPhaseSample, include/vptSamplingFunctions.h:34-47 (g == 0); Henyey-Greenstein
@@ -242,10 +244,9 @@ VPT_DEV dv3 phase_sample(Sampler<COUNT>& smp, dv3 din)
     double xi2 = smp.next();
     double g = smp.g;
     if (g == 0.0) {
-        double theta = vm_acos(1 - 2 * xi1);
         double phi = 2 * VPT_PI * xi2;
         double st, ct, sp, cp;
-        vm_sincos(theta, &st, &ct);
+        vm_sincos_acos(1 - 2 * xi1, &st, &ct);  /* theta = acos(1 - 2 xi1) */
         vm_sincos(phi, &sp, &cp);
         return nrm(mk(st * cp, st * sp, ct));
     }

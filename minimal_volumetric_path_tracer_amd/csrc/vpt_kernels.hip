@@ -282,6 +282,13 @@ __global__ void math_probe_kernel(int fn, const double* x, const double* y, doub
     case 6: r = vm_atan(a); break;
     case 7: r = vm_acos(a); break;
     case 8: r = vm_atan2(a, b); break;
+    case 10:
+    case 11: {
+        double sv, cv;
+        vm_sincos_acos(a, &sv, &cv);
+        r = fn == 10 ? sv : cv;
+        break;
+    }
     default: r = a / b; break;
     }
     out[i] = r;

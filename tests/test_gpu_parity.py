@@ -29,7 +29,7 @@ def _rays(r6):
 # ---------------------------------------------------------------- math library
 @pytest.mark.parametrize("fn,lo,hi", [
     (0, 0, 1e6), (1, -745, 710), (2, 1e-300, 1e300), (3, -7, 7), (4, -7, 7), (5, -1.5, 1.5), (6, -1e3, 1e3),
-    (7, -1, 1), (8, -100, 100), (9, -1e3, 1e3)])
+    (7, -1, 1), (8, -100, 100), (9, -1e3, 1e3), (10, -1, 1), (11, -1, 1)])
 def test_device_math_bitwise(gpu_tracer, orc_vm, fn, lo, hi):
     rng = np.random.default_rng(fn)
     x = rng.uniform(lo, hi, 200000)
