@@ -31,13 +31,23 @@
 
 namespace vpt {
 
-constexpr int POOL = 440;   /* task slots per workgroup (256 lanes): 81 KB of LDS, 2 workgroups/CU */
+#ifndef VPT_POOL_DEBUG
+#define VPT_POOL_DEBUG 0
+#endif
+#ifndef VPT_POOL_WGS
+#define VPT_POOL_WGS 2      /* workgroups per CU (occupancy target; LDS and VGPR budgets follow) */
+#endif
+#ifndef VPT_POOL_SIZE
+#define VPT_POOL_SIZE 440
+#endif
+constexpr int POOL = VPT_POOL_SIZE;  /* task slots per workgroup (256 lanes): 81 KB of LDS at 440 */
 constexpr int NF = 18;      /* doubles per task */
 constexpr int NR = 7;       /* rings */
 constexpr int R_A = 0, R_S = 1, R_M = 5, R_DONE = NR;
 constexpr int URING = 256, UREFILL = 128;  /* work-unit ring: one global queue atomic per 128 units */
 
-/* debug statistics (VPT_POOL_STATS=1, vpt_debug_pool_stats): [0-6] batches per ring, [7-13] lanes
+/* debug statistics, in builds with -DVPT_POOL_DEBUG=1 (scripts/build_variant.sh) run with
+ * VPT_POOL_STATS=1 (vpt_debug_pool_stats, scripts/pool_stats.py): [0-6] batches per ring, [7-13] lanes
  * per ring, [14] idle polls, [15] ticket waits, [16-19] cycles in stage A/S/M/scheduling, [20]
  * stage-A preparation rounds, [21] samples started, [22] cycles preparing, [23] cycles in decide */
 constexpr int NSTATS = 24;
@@ -316,7 +326,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
 }
 
 template <int EST, bool COUNT>
-__global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, const DevScene* __restrict__ S,
+__global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, Medium m, const DevScene* __restrict__ S,
                                                    unsigned long long* counters, unsigned long long* stats)
 {
     __shared__ TaskPool sh;
@@ -345,9 +355,9 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
     smp.cnt.tests = 0;
     smp.cnt.iterations = 0;
     int n = 0, slot = 0, next = R_A;
-    unsigned long long st_idle = 0, st_retry = 0, st_sched = 0;
+    unsigned long long st_idle = 0, st_retry = 0, st_sched = 0, st_b[NR] = {}, st_l[NR] = {}, st_c[3] = {};
     ADbg D = {};
-    const bool dbg = stats != nullptr;
+    const bool dbg = VPT_POOL_DEBUG && stats != nullptr;  /* compiled out of production builds */
     unsigned long long tclk = dbg_clock(dbg);
     while (true) {
         /* ---- an idle wave waits outside the lock until some ring has work (racy peek) ---- */
@@ -435,11 +445,13 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
-        if (dbg) {  /* debug only: per-batch global atomics (no runtime-indexed private arrays) */
-            if (lane == 0) {
-                atomicAdd(&stats[st], 1ull);
-                atomicAdd(&stats[7 + st], (unsigned long long)take);
-            }
+        if (dbg) {  /* debug only; compile-time indices keep the counters in registers */
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+                if (st == r) {
+                    st_b[r] += 1;
+                    st_l[r] += (unsigned long long)take;
+                }
             const unsigned long long now = dbg_clock(dbg);
             st_sched += now - tclk;
             tclk = now;
@@ -470,7 +482,9 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
         }
         if (dbg) {
             const unsigned long long now = dbg_clock(dbg);
-            if (lane == 0) atomicAdd(&stats[16 + stage], now - tclk);
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (stage == k) st_c[k] += now - tclk;
             tclk = now;
         }
     }
@@ -484,6 +498,13 @@ __global__ __launch_bounds__(256, 2) void pool_kernel(PoolParams P, Medium m, co
             atomicAdd(&stats[14], st_idle);
             atomicAdd(&stats[15], st_retry);
             atomicAdd(&stats[19], st_sched);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                atomicAdd(&stats[r], st_b[r]);
+                atomicAdd(&stats[7 + r], st_l[r]);
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) atomicAdd(&stats[16 + k], st_c[k]);
             atomicAdd(&stats[20], D.rounds);
             atomicAdd(&stats[22], D.c_prep);
             atomicAdd(&stats[23], D.c_decide);

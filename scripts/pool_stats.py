@@ -2,6 +2,7 @@
 import ctypes, os, sys, time
 os.environ["VPT_POOL_STATS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("VPT_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build_variants", "libvpt_dbg.so"))
 import minimal_volumetric_path_tracer_amd as vpt
 
 NSTATS = 24
