@@ -333,3 +333,22 @@ def test_alt_scenes_vs_oracle_bitwise(gpu_tracer, orc_vm, samples_alt, scene, es
     assert bitwise_equal(L, Lo).all()
     g = gpu_tracer.render(width=24, height=20, spp=6, estimator=est, seed=SEED, fp64=True)
     assert bitwise_equal(g, orc_vm.render(24, 20, 6, est, seed=SEED)).all()
+
+
+# ---------------------------------------------------------------- pool kernel work hand-out
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,spp,chunk", [
+    (37, 23, 40, 1),    # tile padding (37 x 23 is not a multiple of 8): invalid units are dropped
+    (3, 200, 9, 2),     # narrow image, ragged last chunk (9 = 4 x 2 + 1)
+    (1, 1, 100, 1),     # one pixel, 100 units: one workgroup, the unit ring refilled many times
+    (64, 64, 1, 0),     # 4096 one-sample units over a grid clamped to ceil(4096 / POOL) workgroups
+    (129, 65, 3, 3),    # one chunk per pixel, odd sizes
+])
+def test_pool_work_handout_vs_oracle(gpu_tracer, orc_vm, w, h, spp, chunk):
+    sc = SCENES["default"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    g = gpu_tracer.render(width=w, height=h, spp=spp, chunk_spp=chunk, seed=21, fp64=True)
+    eff = chunk if chunk > 0 else min(spp, 32)
+    o = orc_vm.render(w, h, spp, 0, seed=21, chunk=eff, threads=4)
+    assert g.shape == o.shape and bitwise_equal(g, o).all()
