@@ -377,6 +377,11 @@ VPT_DEV dv3 sph_c(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].
 VPT_DEV dv3 sph_rad(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].radiance); }
 VPT_DEV dv3 sph_p(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].p); }
 
+/* material of sphere `obj`: MK >= 0 when the caller knows it at compile time (the pool kernel's
+ * surface rings are keyed by material), which removes the other materials' code from that path */
+template <int MK>
+VPT_DEV int mat_of(const DevScene* __restrict__ S, int obj) { return MK >= 0 ? MK : S->sph[obj].material; }
+
 /* rayTracer, include/pathTracingUtilities.h:56-64 */
 template <bool COUNT>
 VPT_DEV dv3 ray_tracer(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 x, dv3 wi, int& sourceid)
@@ -472,11 +477,11 @@ VPT_DEV double power_heuristic(double f, double g)
 }
 
 /* MISv2, include/misSamplingFunctions.h:96-170 */
-template <bool COUNT>
+template <bool COUNT, int MK = -1>
 VPT_DEV dv3 mis_v2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray, double alpha,
                    double sigma_t)
 {
-    const int omat = S->sph[obj].material;
+    const int omat = mat_of<MK>(S, obj);
     dv3 mc = mk(0, 0, 0), g;
     dv3 wiLight = mk(0, 0, 0), wiBDRF = mk(0, 0, 0);
     double wg, fpdf = 0, gpdf = 0, cmax = 0;
@@ -590,11 +595,11 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
  * / microfacet), so the draws and directions are taken first in the reference's order, the three
  * rays from x are intersected in one pass (scene_intersect_n), and the arithmetic is then done in
  * the reference's order. */
-template <bool COUNT>
+template <bool COUNT, int MK = -1>
 VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray,
                               double alpha, double sigma_t)
 {
-    const int omat = S->sph[obj].material;
+    const int omat = mat_of<MK>(S, obj);
     const dv3 wo = scl(wray, -1);
     /* ---- draws and directions, in the reference's order */
     int lt[2];
@@ -716,10 +721,10 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
 }
 
 /* bdsf (continuation sample), include/vptShadeMethods.h:16-59 */
-template <bool COUNT>
+template <bool COUNT, int MK = -1>
 VPT_DEV dv3 bdsf(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3& aux, dv3 wray, dv3 n, double& prob, int id)
 {
-    const int mat = S->sph[id].material;
+    const int mat = mat_of<MK>(S, id);
     dv3 wi, fs1 = mk(0, 0, 0);
     dv3 wo = scl(wray, -1);
     if (mat == 0) {
@@ -753,7 +758,7 @@ VPT_DEV dv3 bdsf(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3& aux, 
 }
 
 /* pLight (point-light NEE at a surface), include/vptShadeMethods.h:62-91 */
-template <bool COUNT>
+template <bool COUNT, int MK = -1>
 VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray, int src,
                     double alpha)
 {
@@ -781,7 +786,7 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
     wo = nrm(wo);
     dv3 wh = nrm(add(wi, wo));
     dv3 fr;
-    if (S->sph[obj].material == 1)
+    if (mat_of<MK>(S, obj) == 1)
         fr = fr_microfacet(ld3(S->sph[obj].eta), ld3(S->sph[obj].kappa), wi, wh, wo, alpha, mk(0, 0, 1));
     else
         fr = scl(sph_c(S, obj), (1 / VPT_PI));
@@ -946,7 +951,7 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
 }
 
 /* surface event: point-light NEE (pLight), sphere-light MIS (MISv2), BSDF continuation (bdsf) */
-template <int EST, bool COUNT>
+template <int EST, bool COUNT, int MK = -1>
 VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
                            const Medium& m)
 {
@@ -958,7 +963,7 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     if (EST == 3) {  /* implicit: BSDF continuation only, vptShadeMethods.h:983-994 */
         dv3 wi = mk(0, 0, 0);
         double pdf = 0;
-        dv3 fs = bdsf(S, smp, wi, p.d, nx, pdf, id);
+        dv3 fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
         wi = nrm(wi);
         const double cosine = dot(nx, wi);
         p.beta = scl(scl(scl(mul(p.beta, fs), (1 / continueprob)), cosine), (1 / pdf));
@@ -970,16 +975,16 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     const double probSource = 1.0 / S->n_emit;
     const double alpha = S->sph[id].alpha;
     double Trs = transmitance(xs, sph_p(S, src), sigma_t);
-    dv3 Ldp = scl(scl(p_light(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+    dv3 Ldp = scl(scl(p_light<COUNT, MK>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
 #if VPT_FUSE_RAYS
-    dv3 Ld = S->n_mis == 2 ? mis_v2_two_lights(S, smp, id, xs, nx, p.d, alpha, sigma_t)
-                           : mis_v2(S, smp, id, xs, nx, p.d, alpha, sigma_t);
+    dv3 Ld = S->n_mis == 2 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
+                           : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
 #else
-    dv3 Ld = mis_v2(S, smp, id, xs, nx, p.d, alpha, sigma_t);
+    dv3 Ld = mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
 #endif
     dv3 wi = mk(0, 0, 0);
     double pdf = 0;
-    dv3 fs = bdsf(S, smp, wi, p.d, nx, pdf, id);
+    dv3 fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
     wi = nrm(wi);
     double cosine = dot(nx, wi);
     if (EST == 0) p.L = add(p.L, scl(mul(add(Ldp, Ld), p.beta), (1 / continueprob)));
