@@ -757,14 +757,15 @@ VPT_DEV dv3 bdsf(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3& aux, 
     return fs1;
 }
 
-/* pLight (point-light NEE at a surface), include/vptShadeMethods.h:62-91 */
-template <bool COUNT, int MK = -1>
+/* pLight (point-light NEE at a surface), include/vptShadeMethods.h:62-91.  PT: 1 when the caller
+ * knows the light is a point (r == 0; the pool kernel's rings are keyed by it), -1 unknown. */
+template <bool COUNT, int MK = -1, int PT = -1>
 VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray, int src,
                     double alpha)
 {
     const dv3 I = sph_rad(S, src);
     const dv3 light = sph_p(S, src);
-    const double lr = S->sph[src].r;
+    const double lr = PT == 1 ? 0.0 : S->sph[src].r;
     const bool l3 = S->geo[src].mat3;
     dv3 Le;
     if (visibility(S, smp, light, x, false, lr, l3)) {
@@ -795,15 +796,15 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
 
 /* freeSingleScattering (with_sigma = false), include/volumetricBasicFunctions.h:284-340, and
  * singleScattering (with_sigma = true), :225-281.  din: propagation direction (HG only). */
-template <bool COUNT>
+template <bool COUNT, int LT = -1>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
 VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
                               double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource)
 {
-    const double lr = S->sph[src].r;
+    const double lr = LT == 1 ? 0.0 : S->sph[src].r;
     const dv3 lp = sph_p(S, src);
     const dv3 rad = sph_rad(S, src);
     dv3 Ld = mk(0, 0, 0);
-    if (lr == 0) {
+    if (LT == 1 || (LT < 0 && lr == 0)) {
         if (visibility(S, smp, lp, xt, false, -1.0, false)) {
             double distanceLight = dot(sub(lp, xt), sub(lp, xt));
             dv3 Le = scl(rad, (1 / distanceLight));
@@ -951,7 +952,7 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
 }
 
 /* surface event: point-light NEE (pLight), sphere-light MIS (MISv2), BSDF continuation (bdsf) */
-template <int EST, bool COUNT, int MK = -1>
+template <int EST, bool COUNT, int MK = -1, int PT = -1>  /* MK: material, PT: point light (1), if known */
 VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
                            const Medium& m)
 {
@@ -975,7 +976,7 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     const double probSource = 1.0 / S->n_emit;
     const double alpha = S->sph[id].alpha;
     double Trs = transmitance(xs, sph_p(S, src), sigma_t);
-    dv3 Ldp = scl(scl(p_light<COUNT, MK>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+    dv3 Ldp = scl(scl(p_light<COUNT, MK, PT>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
 #if VPT_FUSE_RAYS
     dv3 Ld = S->n_mis == 2 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
                            : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
@@ -995,8 +996,9 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     p.depth++;
 }
 
-/* medium event: single-scattering NEE toward the picked light, phase-function continuation */
-template <int EST, bool COUNT>
+/* medium event: single-scattering NEE toward the picked light, phase-function continuation.
+ * LT: 1 point light, 0 not, -1 unknown (the pool kernel's medium rings are keyed by it) */
+template <int EST, bool COUNT, int LT = -1>
 VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
                           const Medium& m)
 {
@@ -1015,20 +1017,20 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
     }
     const double probSource = 1.0 / S->n_emit;
     if (EST == 0) {
-        dv3 Ld = single_scattering(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
+        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
         dv3 wi = phase_sample(smp, p.d);
         p.L = add(p.L, scl(scl(mul(Ld, p.beta), (sigma_s / sigma_t)), (1 / continueprob)));
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else if (EST == 2) {  /* vptShadeMethods.h:1252-1258 */
-        dv3 Ld = single_scattering(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
+        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
         dv3 wi = phase_sample(smp, p.d);
         p.L = add(p.L, mul(p.beta, scl(scl(Ld, (sigma_s / sigma_t)), (1 / continueprob))));
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else {
         double T = transmitance(p.o, xt, sigma_t);
-        dv3 Ld = single_scattering(S, smp, xt, p.d, e.src, sigma_t, true, sigma_s, T, probSource);
+        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, true, sigma_s, T, probSource);
         dv3 wi = phase_sample(smp, p.d);
         p.L = add(p.L, mul(p.beta, scl(scl(Ld, (1 / e.pdf)), (1 / continueprob))));
         p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / e.pdf));

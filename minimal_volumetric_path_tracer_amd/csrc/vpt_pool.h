@@ -474,10 +474,17 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
             load_task(sh, slot, t, false);
             smp.X = t.X;
             /* surface rings are keyed by material: diffuse (R_S, R_S+1), metal (R_S+2), other */
-            if (stage == 1 && st <= R_S + 1) surface_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
-            else if (stage == 1 && st == R_S + 2) surface_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
-            else if (stage == 1) surface_event<EST, COUNT, -1>(S, smp, t.p, t.e, m);
-            else medium_event<EST>(S, smp, t.p, t.e, m);
+            /* and by light kind: sphere light (R_S, R_M), point light (R_S + 1, R_M + 1) */
+            if (stage == 1) {
+                if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m);
+                else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
+                else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
+                else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
+            } else if (st == R_M) {
+                medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
+            } else {
+                medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
+            }
             t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
             t.X = smp.X;
             store_task(sh, slot, t, false);
