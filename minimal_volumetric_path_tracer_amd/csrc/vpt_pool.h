@@ -69,12 +69,14 @@ struct TaskPool {
     uint32_t samp[POOL];     /* next sample to start | in_path << 31 */
     uint32_t evw[POOL];      /* depth | id << 16 | src << 24 | killed << 31 */
     uint16_t ring[NR][POOL]; /* slots waiting, per ring */
-    int head[NR], tail[NR];  /* monotonic ring counters */
-    int done;                /* slots retired (work queue exhausted) */
+    /* the scheduler's counters, contiguous so that one lane-parallel LDS read fetches them all:
+     * monotonic ring tails and heads, slots retired, the unit ring's tail, queue exhausted */
+    int ctl[2 * NR + 3];
     int ticket, serving;     /* FIFO ticket lock: a wave returning tasks is never starved */
     uint32_t uring[URING];   /* prefetched work units (refilled under the lock, taken by CAS on uhead) */
-    int uhead, utail, exhausted;
+    int uhead;
 };
+constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_EXH = 2 * NR + 2, NCTL = 2 * NR + 3;
 
 __device__ __forceinline__ int lds_peek(const int* p)
 {
@@ -228,11 +230,11 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             const int k = __popcll(needm);
             int h = 0, got = 0, ex = 0;
             if (lane == leader) {  /* take up to k units from the workgroup's ring */
-                ex = __hip_atomic_load(&sh.exhausted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                ex = __hip_atomic_load(&sh.ctl[C_EXH], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 h = lds_peek(&sh.uhead);
                 while (true) {
                     const int avail =
-                        __hip_atomic_load(&sh.utail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - h;
+                        __hip_atomic_load(&sh.ctl[C_UTAIL], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - h;
                     got = min(k, avail);
                     if (got <= 0) {
                         got = 0;
@@ -338,14 +340,10 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
         sh.evw[j] = 0;
         sh.ring[R_A][j] = (uint16_t)j;
     }
-    if (tid < NR) {
-        sh.head[tid] = 0;
-        sh.tail[tid] = tid == R_A ? POOL : 0;
-    }
+    if (tid < NCTL) sh.ctl[tid] = tid == C_TAIL + R_A ? POOL : 0;  /* every slot starts in ring A */
     if (tid == 0) {
-        sh.done = 0;
         sh.ticket = sh.serving = 0;
-        sh.uhead = sh.utail = sh.exhausted = 0;
+        sh.uhead = 0;
     }
     __syncthreads();
 
@@ -364,11 +362,13 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
         if (n == 0) {
             bool fin = false;
             while (true) {
+                const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
                 int pend = 0;
 #pragma unroll
-                for (int r = 0; r < NR; ++r) pend += lds_peek(&sh.tail[r]) - lds_peek(&sh.head[r]);
-                if (__builtin_amdgcn_readfirstlane(pend) > 0) break;
-                if (__builtin_amdgcn_readfirstlane(lds_peek(&sh.done)) == POOL) {
+                for (int r = 0; r < NR; ++r)
+                    pend += __builtin_amdgcn_readlane(v, C_TAIL + r) - __builtin_amdgcn_readlane(v, C_HEAD + r);
+                if (pend > 0) break;
+                if (__builtin_amdgcn_readlane(v, C_DONE) == POOL) {
                     fin = true;
                     break;
                 }
@@ -387,44 +387,49 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        /* all counters in one LDS read (lane k holds ctl[k]); positions, counts and the choice of
+         * ring are then worked out in registers, and the updates go back in two LDS writes */
+        int cv = lane < NCTL ? sh.ctl[lane] : 0;
         if (n > 0) {
+            const bool ret = lane < n && next < NR;
+            int pos = 0;
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                const bool mine = lane < n && next == r;
-                const uint64_t msk = __ballot(mine);
+                const uint64_t msk = __ballot(ret && next == r);
                 if (msk) {
-                    const int base = sh.tail[r];
-                    if (mine) sh.ring[r][(base + __popcll(msk & below)) % POOL] = (uint16_t)slot;
-                    if (lane == 0) sh.tail[r] = base + __popcll(msk);
+                    const int tr = __builtin_amdgcn_readlane(cv, C_TAIL + r);
+                    if (ret && next == r) pos = tr + __popcll(msk & below);
+                    if (lane == C_TAIL + r) cv = tr + __popcll(msk);
                 }
             }
+            if (ret) sh.ring[next][pos % POOL] = (uint16_t)slot;
             const uint64_t md = __ballot(lane < n && next == R_DONE);
-            if (lane == 0 && md) sh.done += __popcll(md);
+            if (lane == C_DONE) cv += __popcll(md);
+            if (lane <= C_DONE) sh.ctl[lane] = cv;  /* tails, heads (unchanged), done */
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         /* keep the unit ring stocked: the queue atomic's latency is paid here once per 128 units
          * instead of in every stage-A round (all waves on the chip contend for that address) */
-        if (!__builtin_amdgcn_readfirstlane(sh.exhausted) &&
-            __builtin_amdgcn_readfirstlane(sh.utail - lds_peek(&sh.uhead)) < UREFILL) {
+        if (!__builtin_amdgcn_readlane(cv, C_EXH) &&
+            __builtin_amdgcn_readlane(cv, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL) {
             unsigned base = 0;
             if (lane == 0) base = atomicAdd(P.queue, (unsigned)UREFILL);
             base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
             const unsigned left = base < P.nunits ? P.nunits - base : 0u;
             const int nv = (int)(left < (unsigned)UREFILL ? left : (unsigned)UREFILL);
-            const int t0 = sh.utail;
+            const int t0 = __builtin_amdgcn_readlane(cv, C_UTAIL);
             for (int j = lane; j < nv; j += 64) sh.uring[(t0 + j) % URING] = base + (unsigned)j;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) {
-                __hip_atomic_store(&sh.utail, t0 + nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&sh.ctl[C_UTAIL], t0 + nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (left <= (unsigned)UREFILL)
-                    __hip_atomic_store(&sh.exhausted, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&sh.ctl[C_EXH], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
-        const int done = __builtin_amdgcn_readfirstlane(sh.done);
+        const int done = __builtin_amdgcn_readlane(cv, C_DONE);
         int st = 0, best = -1;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            const int c = __builtin_amdgcn_readfirstlane(sh.tail[r] - sh.head[r]);
+            const int c = __builtin_amdgcn_readlane(cv, C_TAIL + r) - __builtin_amdgcn_readlane(cv, C_HEAD + r);
             if (c > best) {
                 best = c;
                 st = r;
@@ -432,9 +437,9 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
         }
         const int take = min(64, best);
         if (take > 0) {
-            const int h0 = sh.head[st];
+            const int h0 = __builtin_amdgcn_readlane(cv, C_HEAD + st);
             if (lane < take) slot = sh.ring[st][(h0 + lane) % POOL];
-            if (lane == 0) sh.head[st] = h0 + take;
+            if (lane == 0) sh.ctl[C_HEAD + st] = h0 + take;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&sh.serving, ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
