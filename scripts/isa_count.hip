@@ -129,38 +129,72 @@ extern "C" __global__ void k_phase_sample(double* in, double* out, uint64_t* X)
     out[threadIdx.x] = v.x + v.y + v.z;
 }
 
-extern "C" __global__ void k_stage_a(PoolParams P, const DevScene* S, double* in, double* out, uint64_t* X)
+/* specialised stage bodies as the pool kernel instantiates them */
+template <int MK, int PT>
+__device__ __forceinline__ void run_surface(const DevScene* S, double* in, double* out, uint64_t* X)
 {
     Sampler<false> smp;
     smp.X = X[threadIdx.x];
     smp.g = in[100];
     Medium m{in[101], in[102], in[103], (int)in[104]};
-    Task t;
-    t.p.o = IN3(in, threadIdx.x);
-    t.p.d = IN3(in, threadIdx.x + 3);
-    t.p.beta = IN3(in, threadIdx.x + 6);
-    t.p.L = IN3(in, threadIdx.x + 9);
-    t.p.depth = (int)in[threadIdx.x + 12];
-    t.acc = IN3(in, threadIdx.x + 13);
-    t.unit = (unsigned)in[threadIdx.x + 16];
-    t.i = (unsigned)in[threadIdx.x + 17];
-    t.in_path = in[threadIdx.x + 18] > 0;
-    t.X = X[threadIdx.x + 64];
-    ADbg D;
-    const int lane = threadIdx.x & 63;
-    int r = stage_a<0, false>(P, S, m, smp, t, threadIdx.x < in[0], lane, (1ull << lane) - 1ull, false, D);
-    out[threadIdx.x] = t.p.L.x + t.p.L.y + t.p.beta.z + t.p.d.x + t.p.o.y + t.e.dist + r + t.acc.x + t.i;
-    X[threadIdx.x] = t.X;
+    Path p;
+    p.o = IN3(in, threadIdx.x);
+    p.d = IN3(in, threadIdx.x + 3);
+    p.beta = IN3(in, threadIdx.x + 6);
+    p.L = IN3(in, threadIdx.x + 9);
+    p.depth = (int)in[threadIdx.x + 12];
+    Event e;
+    e.t = in[threadIdx.x + 13];
+    e.dist = in[threadIdx.x + 14];
+    e.pdf = in[threadIdx.x + 15];
+    e.id = (int)in[threadIdx.x + 16];
+    e.src = (int)in[threadIdx.x + 17];
+    surface_event<0, false, MK, PT>(S, smp, p, e, m);
+    out[threadIdx.x] = p.L.x + p.L.y + p.beta.z + p.d.x + p.o.y;
+    X[threadIdx.x] = smp.X;
 }
-extern "C" __global__ void k_decode_unit(PoolParams P, const unsigned* in, unsigned* out)
-{
-    Unit u = decode_unit(P, in[threadIdx.x]);
-    out[threadIdx.x] = u.x + u.y + u.c + (unsigned)u.idx + u.lr + u.valid;
-}
-extern "C" __global__ void k_camera(PoolParams P, const int* in, double* out, uint64_t* X)
+extern "C" __global__ void k_surface_diffuse_sphere(const DevScene* S, double* in, double* out, uint64_t* X) { run_surface<0, 0>(S, in, out, X); }
+extern "C" __global__ void k_surface_diffuse_point(const DevScene* S, double* in, double* out, uint64_t* X) { run_surface<0, 1>(S, in, out, X); }
+extern "C" __global__ void k_mis_v2_diffuse(const DevScene* S, double* in, double* out, uint64_t* X)
 {
     Sampler<false> smp;
     smp.X = X[threadIdx.x];
-    dv3 v = pool_camera_dir(P, smp, in[threadIdx.x], in[threadIdx.x + 1]);
+    dv3 v = mis_v2<false, 0>(S, smp, (int)in[0], IN3(in, threadIdx.x), IN3(in, threadIdx.x + 3), IN3(in, threadIdx.x + 6), in[2], in[3]);
     out[threadIdx.x] = v.x + v.y + v.z;
+}
+extern "C" __global__ void k_p_light_diffuse(const DevScene* S, double* in, double* out, uint64_t* X)
+{
+    Sampler<false> smp;
+    smp.X = X[threadIdx.x];
+    dv3 v = p_light<false, 0, 0>(S, smp, (int)in[0], IN3(in, threadIdx.x), IN3(in, threadIdx.x + 3), IN3(in, threadIdx.x + 6),
+                                 (int)in[1], in[2]);
+    out[threadIdx.x] = v.x + v.y + v.z;
+}
+extern "C" __global__ void k_bdsf_diffuse(const DevScene* S, double* in, double* out, uint64_t* X)
+{
+    Sampler<false> smp;
+    smp.X = X[threadIdx.x];
+    dv3 aux;
+    double prob;
+    dv3 v = bdsf<false, 0>(S, smp, aux, IN3(in, threadIdx.x), IN3(in, threadIdx.x + 3), prob, (int)in[0]);
+    out[threadIdx.x] = v.x + v.y + v.z + aux.x + prob;
+}
+extern "C" __global__ void k_medium_sphere(const DevScene* S, double* in, double* out, uint64_t* X)
+{
+    Sampler<false> smp;
+    smp.X = X[threadIdx.x];
+    smp.g = in[100];
+    Medium m{in[101], in[102], in[103], (int)in[104]};
+    Path p;
+    p.o = IN3(in, threadIdx.x);
+    p.d = IN3(in, threadIdx.x + 3);
+    p.beta = IN3(in, threadIdx.x + 6);
+    p.L = IN3(in, threadIdx.x + 9);
+    p.depth = 0;
+    Event e;
+    e.dist = in[threadIdx.x + 14];
+    e.src = (int)in[threadIdx.x + 17];
+    medium_event<0, false, 0>(S, smp, p, e, m);
+    out[threadIdx.x] = p.L.x + p.L.y + p.beta.z + p.d.x + p.o.y;
+    X[threadIdx.x] = smp.X;
 }
