@@ -40,6 +40,12 @@ namespace vpt {
 #ifndef VPT_POOL_SIZE
 #define VPT_POOL_SIZE 440
 #endif
+#ifndef VPT_SCHED_PRIO
+#define VPT_SCHED_PRIO 3    /* s_setprio level of the scheduler's critical section (0: off; A/B 3 vs 0: +0.7 %) */
+#endif
+#ifndef VPT_PREP_ROUNDS
+#define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s) */
+#endif
 constexpr int POOL = VPT_POOL_SIZE;  /* task slots per workgroup (256 lanes): 81 KB of LDS at 440 */
 constexpr int NF = 18;      /* doubles per task */
 constexpr int NR = 7;       /* rings */
@@ -221,8 +227,10 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         t.killed = false;
     }
     const unsigned long long c0 = dbg_clock(dbg);
+    int round = 0;
     while (true) {
         if (dbg) ++D.rounds;
+        ++round;
         const bool need = !done && !parked && t.c1 == 0;
         const uint64_t needm = __ballot(need);
         if (needm) {
@@ -289,6 +297,13 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             }
         }
         if (__ballot(!done && !parked && !t.in_path) == 0) break;
+        /* a lane still without a path after VPT_PREP_ROUNDS rounds is parked (back to ring A, it
+         * continues from its next sample in a later batch) instead of holding the whole wave in
+         * this loop: the wave's round count is the maximum over its lanes of a geometric count */
+        if (VPT_PREP_ROUNDS > 0 && round >= VPT_PREP_ROUNDS) {
+            if (!done && !t.in_path) parked = true;
+            break;
+        }
     }
     if (fresh) {  /* camera ray of the surviving sample: src/rt.cpp:787-789 */
         smp.X = t.X;
@@ -379,6 +394,10 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
         }
         /* ---- critical section: return finished tasks, take a batch of the fullest ring ---- */
         int ticket = 0;
+        /* the critical section runs at raised issue priority: VALU issue between the two waves of
+         * a SIMD goes by priority, then age, and a lock holder starved by a computing partner wave
+         * holds up every other wave of its workgroup */
+        if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(VPT_SCHED_PRIO);
         if (lane == 0) {
             ticket = __hip_atomic_fetch_add(&sh.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             while (lds_peek(&sh.serving) != ticket) {
@@ -443,6 +462,7 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&sh.serving, ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(0);
         n = take;
         if (done == POOL) break;
         if (take == 0) {

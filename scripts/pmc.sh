@@ -15,7 +15,10 @@ PASSES=(
   "SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_SALU SQ_LEVEL_WAVES"
   "FETCH_SIZE"
   "WRITE_SIZE"
+  "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_IFETCH_LEVEL SQ_INSTS_VALU SQ_WAVES"
 )
+# PMC_PASSES="A B;C D" replaces the list (one pass per ';'-separated group)
+if [ -n "${PMC_PASSES:-}" ]; then IFS=';' read -r -a PASSES <<< "$PMC_PASSES"; fi
 i=0
 for p in "${PASSES[@]}"; do
     i=$((i + 1))

@@ -53,6 +53,27 @@ def test_device_sqrt_div_correctly_rounded(gpu_tracer, orc):
     assert bitwise_equal(gpu_tracer.math_probe(9, x, y), x / y).all()
 
 
+def test_device_sqrt_edges(gpu_tracer):
+    """vm_sqrt's unwrapped fast path covers [2^-767, DBL_MAX]; everything else (and the range
+    ends) must give sqrt()'s bits too: zeros, subnormals, the 2^-767 boundary, inf, NaN,
+    negatives, exact squares and their neighbours."""
+    rng = np.random.default_rng(11)
+    b = 2.0 ** -767
+    edge = [0.0, -0.0, 5e-324, 2.2250738585072014e-308, np.nextafter(b, 0), b, np.nextafter(b, 1),
+            1.7976931348623157e308, np.inf, -np.inf, np.nan, -1.0, -5e-324, 1.0, 4.0, 2.0]
+    sq = rng.uniform(1, 2 ** 26, 20000).round() ** 2
+    near = np.concatenate([sq, np.nextafter(sq, 0), np.nextafter(sq, np.inf)])
+    tiny = rng.uniform(0.5, 2, 20000) * 2.0 ** rng.integers(-1074, -700, 20000)
+    big = rng.uniform(0.5, 2, 20000) * 2.0 ** rng.integers(900, 1024, 20000)
+    x = np.concatenate([edge, near, tiny, big, -tiny])
+    with np.errstate(invalid="ignore", over="ignore"):
+        ref = np.sqrt(x)
+    dev = gpu_tracer.math_probe(0, x)
+    same = (dev.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(dev) & np.isnan(ref))  # signed zeros too
+    assert same.all(), f"{(~same).sum()} differ, e.g. x={x[~same][:3]}"
+
+
+
 # ---------------------------------------------------------------- per-sample estimator
 @pytest.fixture(scope="module")
 def samples():
