@@ -43,6 +43,9 @@ namespace vpt {
 #ifndef VPT_SCHED_PRIO
 #define VPT_SCHED_PRIO 3    /* s_setprio level of the scheduler's critical section (0: off; A/B 3 vs 0: +0.7 %) */
 #endif
+#ifndef VPT_FUSE_A
+#define VPT_FUSE_A 1        /* stage A run by the S/M wave on its own batch (0: via ring A) */
+#endif
 #ifndef VPT_PREP_ROUNDS
 #define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s) */
 #endif
@@ -495,25 +498,39 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
             }
             next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbg, D);
             if (active) store_task(sh, slot, t, true);
-        } else if (active) {
-            load_task(sh, slot, t, false);
-            smp.X = t.X;
-            /* surface rings are keyed by material: diffuse (R_S, R_S+1), metal (R_S+2), other */
-            /* and by light kind: sphere light (R_S, R_M), point light (R_S + 1, R_M + 1) */
-            if (stage == 1) {
-                if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m);
-                else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
-                else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
-                else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
-            } else if (st == R_M) {
-                medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
+        } else {
+            if (active) {
+                load_task(sh, slot, t, VPT_FUSE_A != 0);
+                smp.X = t.X;
+                /* surface rings are keyed by material: diffuse (R_S, R_S+1), metal (R_S+2), other */
+                /* and by light kind: sphere light (R_S, R_M), point light (R_S + 1, R_M + 1) */
+                if (stage == 1) {
+                    if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m);
+                    else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
+                    else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
+                    else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
+                } else if (st == R_M) {
+                    medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
+                } else {
+                    medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
+                }
+                t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
+                t.X = smp.X;
             } else {
-                medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
+                t.c1 = 0;
+                t.in_path = false;
+                t.killed = false;
             }
-            t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
-            t.X = smp.X;
-            store_task(sh, slot, t, false);
+#if VPT_FUSE_A
+            /* every task leaving S/M goes to stage A: the same wave runs it on the same lanes
+             * right away, instead of storing the batch, returning it to ring A under the lock and
+             * loading it again in another wave */
+            next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbg, D);
+            if (active) store_task(sh, slot, t, true);
+#else
+            if (active) store_task(sh, slot, t, false);
             next = R_A;
+#endif
         }
         if (dbg) {
             const unsigned long long now = dbg_clock(dbg);
