@@ -32,11 +32,11 @@
 #ifndef VPT_ISECT_UNROLL
 #define VPT_ISECT_UNROLL 5
 #endif
-/* rays from the surface point intersected in one pass by MISv2 (0 = off, 2, 3): bit-exact, but
- * measured slower in the pool kernel (off / 2 / 3: 4148 / 4036 / 4063 Ms/s) -- the extra live
- * registers spill at 256 VGPRs; kept for a kernel with a separate surface-stage register budget */
+/* rays from the surface point intersected in one pass by MISv2 (0 = off, 2, 3): bit-exact.  Slower
+ * before stage A was fused into the S/M wave (off / 2 / 3: 4148 / 4036 / 4063 Ms/s, spills at 256
+ * VGPRs), faster since (off / 2 / 3: 5584 / 5569 / 5609) */
 #ifndef VPT_FUSE_RAYS
-#define VPT_FUSE_RAYS 0
+#define VPT_FUSE_RAYS 3
 #endif
 /* sphere loops taken G spheres at a time (scene_intersect_grouped): decide() and every other
  * site; A/B at 1024^2 x 256: off 4914, decide only G=5 4967 (G=10 4857), all sites G=5 5042, G=3 5009 */
