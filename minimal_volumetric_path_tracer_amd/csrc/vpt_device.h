@@ -46,6 +46,16 @@
 
 namespace vpt {
 
+/* timing experiment only (NOT bit-exact): the intersection tests' square roots approximated */
+#ifndef VPT_ISECT_SQRT_APPROX
+#define VPT_ISECT_SQRT_APPROX 0
+#endif
+#if VPT_ISECT_SQRT_APPROX
+#define ISECT_SQRT(x) ((x) * __builtin_amdgcn_rsq(x))
+#else
+#define ISECT_SQRT(x) vm_sqrt(x)
+#endif
+
 /* ------------------------------------------------------------------ vectors (Vector.h:10-36) */
 struct dv3 {
     double x, y, z;
@@ -101,7 +111,7 @@ VPT_DEV int scene_intersect(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
         double det = b * b - cc + g.r2;
         double tact = 0.0;
         if (det >= 0) {
-            double sq = vm_sqrt(det);
+            double sq = ISECT_SQRT(det);
             double t2 = -b + sq;
             double t1 = -b - sq;
             tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
@@ -148,7 +158,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         for (int k = 0; k < G; ++k) {
             double tact = 0.0;
             if (det[k] >= 0) {
-                const double sq = vm_sqrt(det[k]);
+                const double sq = ISECT_SQRT(det[k]);
                 const double t2 = -b[k] + sq;
                 const double t1 = -b[k] - sq;
                 tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
@@ -170,7 +180,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         const double det = b * b - cc + g.r2;
         double tact = 0.0;
         if (det >= 0) {
-            const double sq = vm_sqrt(det);
+            const double sq = ISECT_SQRT(det);
             const double t2 = -b + sq;
             const double t1 = -b - sq;
             tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
@@ -278,7 +288,7 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
         double det = b * b - (ocx * ocx + ocy * ocy + ocz * ocz) + g.r2;
         double ta = 0.0, tb = 0.0;
         if (!(det < 0)) {
-            double sq = vm_sqrt(det);
+            double sq = ISECT_SQRT(det);
             tb = -b + sq;
             ta = -b - sq;
         }
@@ -655,7 +665,7 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
             const double det = b * b - cc + g.r2;
             double tact = 0.0;
             if (det >= 0) {
-                const double sq = vm_sqrt(det);
+                const double sq = ISECT_SQRT(det);
                 const double t2 = -b + sq;
                 const double t1 = -b - sq;
                 tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
@@ -883,7 +893,12 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
 }
 
 /* freeSingleScattering (with_sigma = false), include/volumetricBasicFunctions.h:284-340, and
- * singleScattering (with_sigma = true), :225-281.  din: propagation direction (HG only). */
+ * singleScattering (with_sigma = true), :225-281.  din: propagation direction (HG only).
+ * For a point light the reference first casts the shadow ray (:295-304 / :236-245), then the cone
+ * ray (:310-337), whose result REPLACES Ld whenever the cone ray's first hit is the light (SURVEY
+ * H5: 80-87 % of point-light events).  The shadow ray draws nothing, so it is cast after the cone
+ * ray here and only when its result survives: same draws, same bits, one ray cast fewer in most
+ * point-light medium events (counting mode still adds its tests). */
 template <bool COUNT, int LT = -1>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
 VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
                               double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource)
@@ -891,17 +906,8 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     const double lr = LT == 1 ? 0.0 : S->sph[src].r;
     const dv3 lp = sph_p(S, src);
     const dv3 rad = sph_rad(S, src);
+    const bool point = LT == 1 || (LT < 0 && lr == 0);
     dv3 Ld = mk(0, 0, 0);
-    if (LT == 1 || (LT < 0 && lr == 0)) {
-        if (visibility(S, smp, lp, xt, false, -1.0, false)) {
-            double distanceLight = dot(sub(lp, xt), sub(lp, xt));
-            dv3 Le = scl(rad, (1 / distanceLight));
-            double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, nrm(sub(lp, xt)));
-            dv3 Ls = scl(scl(Le, transmitance(xt, lp, sigma_t)), ph);
-            if (with_sigma) Ld = scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
-            else Ld = scl(Ls, (1 / probSource));
-        }
-    }
     dv3 wc = sub(lp, xt);
     double mag = vm_sqrt(dot(wc, wc));
     wc = scl(wc, (1 / mag));
@@ -912,11 +918,21 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     int idHit = 0;
     scene_isect(S, smp, xt, wl, tdist, idHit, false);
     if (src == idHit) {
+        if (point) smp.tests(S->n);  /* the shadow ray the reference casts first (result overwritten) */
         double it = vm_exp(sigma_t * tdist * -1.0);
         double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, wl);
         dv3 Ls = scl(scl(rad, it), ph);
         if (with_sigma) Ld = scl(scl(scl(scl(Ls, trxt), sigma_s), (1 / prob_wl)), (1 / probSource));
         else Ld = scl(scl(Ls, (1 / prob_wl)), (1 / probSource));
+    } else if (point) {
+        if (visibility(S, smp, lp, xt, false, -1.0, false)) {
+            double distanceLight = dot(sub(lp, xt), sub(lp, xt));
+            dv3 Le = scl(rad, (1 / distanceLight));
+            double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, nrm(sub(lp, xt)));
+            dv3 Ls = scl(scl(Le, transmitance(xt, lp, sigma_t)), ph);
+            if (with_sigma) Ld = scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
+            else Ld = scl(Ls, (1 / probSource));
+        }
     }
     return Ld;
 }
