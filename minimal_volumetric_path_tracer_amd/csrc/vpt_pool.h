@@ -46,6 +46,9 @@ namespace vpt {
 #ifndef VPT_FUSE_A
 #define VPT_FUSE_A 1        /* stage A run by the S/M wave on its own batch (0: via ring A) */
 #endif
+#ifndef VPT_LOCKFREE
+#define VPT_LOCKFREE 1      /* rings without the ticket lock (ring_entry) */
+#endif
 #ifndef VPT_PREP_ROUNDS
 #define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s) */
 #endif
@@ -55,7 +58,8 @@ constexpr int NR = 7;       /* rings */
 constexpr int R_A = 0, R_S = 1, R_M = 5, R_DONE = NR;
 constexpr int URING = 256, UREFILL = 128;  /* work-unit ring: one global queue atomic per 128 units */
 
-/* debug statistics, in builds with -DVPT_POOL_DEBUG=1 (scripts/build_variant.sh) run with
+/* debug statistics, in builds with -DVPT_POOL_DEBUG=1 (=2: top-level cycle split only, cheaper;
+ * scripts/build_variant.sh) run with
  * VPT_POOL_STATS=1 (vpt_debug_pool_stats, scripts/pool_stats.py): [0-6] batches per ring, [7-13] lanes
  * per ring, [14] idle polls, [15] ticket waits, [16-19] cycles in stage A/S/M/scheduling, [20]
  * stage-A preparation rounds, [21] samples started, [22] cycles preparing, [23] cycles in decide */
@@ -85,7 +89,21 @@ struct TaskPool {
     uint32_t uring[URING];   /* prefetched work units (refilled under the lock, taken by CAS on uhead) */
     int uhead;
 };
-constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_EXH = 2 * NR + 2, NCTL = 2 * NR + 3;
+constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_EXH = 2 * NR + 2, C_RFL = 2 * NR + 3,
+              NCTL = 2 * NR + 4;
+
+/* Lock-free rings (VPT_LOCKFREE): an entry is the slot and the lap of its ring position,
+ * slot | (position / POOL mod 128) << 9.  A producer reserves positions with one atomic add on the
+ * ring's tail and then writes the entries; a consumer reads entries from the head, keeps the prefix
+ * whose lap tags are current (written), and claims exactly that prefix with one CAS on the head.
+ * An entry is read before the claim, and its position cannot be reserved again before the claim
+ * (tail - head < POOL), so a claimed entry is never a later lap's. */
+constexpr int SLOT_BITS = 9, SLOT_MASK = (1 << SLOT_BITS) - 1, LAP_MASK = 127;
+static_assert(POOL <= (1 << SLOT_BITS), "slot ids must fit the ring entry");
+__device__ __forceinline__ uint16_t ring_entry(int slot, int pos)
+{
+    return (uint16_t)(slot | (((pos / POOL) & LAP_MASK) << SLOT_BITS));
+}
 
 __device__ __forceinline__ int lds_peek(const int* p)
 {
@@ -356,7 +374,8 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
         sh.c1[j] = 0;
         sh.samp[j] = 0;
         sh.evw[j] = 0;
-        sh.ring[R_A][j] = (uint16_t)j;
+        sh.ring[R_A][j] = (uint16_t)j;  /* = ring_entry(j, j): lap 0 */
+        for (int r = 1; r < NR; ++r) sh.ring[r][j] = (uint16_t)(LAP_MASK << SLOT_BITS);  /* no lap-0 entry yet */
     }
     if (tid < NCTL) sh.ctl[tid] = tid == C_TAIL + R_A ? POOL : 0;  /* every slot starts in ring A */
     if (tid == 0) {
@@ -374,8 +393,123 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
     unsigned long long st_idle = 0, st_retry = 0, st_sched = 0, st_b[NR] = {}, st_l[NR] = {}, st_c[3] = {};
     ADbg D = {};
     const bool dbg = VPT_POOL_DEBUG && stats != nullptr;  /* compiled out of production builds */
+    const bool dbga = VPT_POOL_DEBUG == 1 && dbg;          /* stage-A internals (VPT_POOL_DEBUG=2: top level only) */
     unsigned long long tclk = dbg_clock(dbg);
     while (true) {
+#if VPT_LOCKFREE
+        /* ---- scheduling without a lock (ring_entry): reserve, publish, claim ---- */
+        if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(VPT_SCHED_PRIO);
+        if (n > 0) {  /* return the finished tasks: one LDS atomic per ring reserves their positions */
+            const bool ret = lane < n && next < NR;
+            int rank = 0, cnt = 0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const uint64_t msk = __ballot(ret && next == r);
+                if (ret && next == r) rank = __popcll(msk & below);
+                if (lane == r) cnt = __popcll(msk);
+            }
+            int base = 0;
+            if (lane < NR && cnt > 0)
+                base = __hip_atomic_fetch_add(&sh.ctl[C_TAIL + lane], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int pos = __shfl(base, ret ? next : 0) + rank;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  /* task states before their entries */
+            if (ret) ((volatile uint16_t*)sh.ring[next])[pos % POOL] = ring_entry(slot, pos);
+            const uint64_t md = __ballot(lane < n && next == R_DONE);
+            if (md && lane == 0)
+                __hip_atomic_fetch_add(&sh.ctl[C_DONE], __popcll(md), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        /* keep the unit ring stocked (the queue atomic's latency is paid once per 128 units); one
+         * wave at a time, claimed by a flag */
+        {
+            const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+            if (!__builtin_amdgcn_readlane(v, C_EXH) && !__builtin_amdgcn_readlane(v, C_RFL) &&
+                __builtin_amdgcn_readlane(v, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL) {
+                int own = 0;
+                if (lane == 0) {
+                    int z = 0;
+                    own = __hip_atomic_compare_exchange_strong(&sh.ctl[C_RFL], &z, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                if (__builtin_amdgcn_readfirstlane(own)) {
+                    const int t0 = __builtin_amdgcn_readfirstlane(lds_peek(&sh.ctl[C_UTAIL]));
+                    if (t0 - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL) {
+                        unsigned ubase = 0;
+                        if (lane == 0) ubase = atomicAdd(P.queue, (unsigned)UREFILL);
+                        ubase = (unsigned)__builtin_amdgcn_readfirstlane((int)ubase);
+                        const unsigned left = ubase < P.nunits ? P.nunits - ubase : 0u;
+                        const int nv = (int)(left < (unsigned)UREFILL ? left : (unsigned)UREFILL);
+                        for (int j = lane; j < nv; j += 64) sh.uring[(t0 + j) % URING] = ubase + (unsigned)j;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        if (lane == 0) {
+                            __hip_atomic_store(&sh.ctl[C_UTAIL], t0 + nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (left <= (unsigned)UREFILL)
+                                __hip_atomic_store(&sh.ctl[C_EXH], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    }
+                    if (lane == 0) __hip_atomic_store(&sh.ctl[C_RFL], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+        /* take a batch of the fullest ring: read its published entries, then claim them by one CAS
+         * on the ring's head (a claim never covers an entry that is not yet written) */
+        int st = 0, take = 0;
+        bool fin = false;
+        while (true) {
+            const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+            int best = 0;
+            st = 0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int c = __builtin_amdgcn_readlane(v, C_TAIL + r) - __builtin_amdgcn_readlane(v, C_HEAD + r);
+                if (c > best) {
+                    best = c;
+                    st = r;
+                }
+            }
+            if (best <= 0) {
+                if (__builtin_amdgcn_readlane(v, C_DONE) == POOL) {
+                    fin = true;
+                    break;
+                }
+                ++st_idle;
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            const int h = __builtin_amdgcn_readlane(v, C_HEAD + st);
+            const int want = min(64, best);
+            int e = 0;
+            bool ok = false;
+            if (lane < want) {
+                const int p = h + lane;
+                e = ((volatile uint16_t*)sh.ring[st])[p % POOL];
+                ok = (e >> SLOT_BITS) == ((p / POOL) & LAP_MASK);
+            }
+            const uint64_t okm = __ballot(ok);
+            const int got = okm == ~0ull ? 64 : __builtin_ctzll(~okm);  /* the published prefix */
+            if (got == 0) {
+                ++st_retry;
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            int won = 0;
+            if (lane == 0) {
+                int hh = h;
+                won = __hip_atomic_compare_exchange_strong(&sh.ctl[C_HEAD + st], &hh, h + got, __ATOMIC_RELAXED,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (!__builtin_amdgcn_readfirstlane(won)) {
+                ++st_retry;
+                continue;
+            }
+            take = got;
+            slot = e & SLOT_MASK;
+            break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  /* the claimed tasks' states */
+        if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (fin) break;
+        n = take;
+#else
         /* ---- an idle wave waits outside the lock until some ring has work (racy peek) ---- */
         if (n == 0) {
             bool fin = false;
@@ -473,6 +607,7 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
+#endif
         if (dbg) {  /* debug only; compile-time indices keep the counters in registers */
 #pragma unroll
             for (int r = 0; r < NR; ++r)
@@ -496,7 +631,7 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
                 t.in_path = false;
                 t.killed = false;
             }
-            next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbg, D);
+            next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
             if (active) store_task(sh, slot, t, true);
         } else {
             if (active) {
@@ -525,7 +660,7 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
             /* every task leaving S/M goes to stage A: the same wave runs it on the same lanes
              * right away, instead of storing the batch, returning it to ring A under the lock and
              * loading it again in another wave */
-            next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbg, D);
+            next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
             if (active) store_task(sh, slot, t, true);
 #else
             if (active) store_task(sh, slot, t, false);
