@@ -43,6 +43,14 @@
 #ifndef VPT_DECIDE_GROUP
 #define VPT_DECIDE_GROUP 5
 #endif
+/* square roots of the intersection tests computed branch-free (sqrt of max(det, 0), result selected)
+ * in the grouped loop (G) and in the fused multi-ray loop (N), so that independent chains overlap */
+#ifndef VPT_BF_G
+#define VPT_BF_G 0
+#endif
+#ifndef VPT_BF_N
+#define VPT_BF_N 0
+#endif
 
 namespace vpt {
 
@@ -157,7 +165,12 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             double tact = 0.0;
-            if (det[k] >= 0) {
+            if (VPT_BF_G) {  /* branch-free: the G square-root chains overlap (same values where det >= 0) */
+                const double sq = ISECT_SQRT(det[k] >= 0 ? det[k] : 0.0);
+                const double t2 = -b[k] + sq;
+                const double t1 = -b[k] - sq;
+                tact = det[k] >= 0 ? ((t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1) : 0.0;
+            } else if (det[k] >= 0) {
                 const double sq = ISECT_SQRT(det[k]);
                 const double t2 = -b[k] + sq;
                 const double t1 = -b[k] - sq;
@@ -664,7 +677,12 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
             const double b = ocx * d[k].x + ocy * d[k].y + ocz * d[k].z;
             const double det = b * b - cc + g.r2;
             double tact = 0.0;
-            if (det >= 0) {
+            if (VPT_BF_N) {  /* branch-free: the N rays' square-root chains overlap */
+                const double sq = ISECT_SQRT(det >= 0 ? det : 0.0);
+                const double t2 = -b + sq;
+                const double t1 = -b - sq;
+                tact = det >= 0 ? ((t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1) : 0.0;
+            } else if (det >= 0) {
                 const double sq = ISECT_SQRT(det);
                 const double t2 = -b + sq;
                 const double t1 = -b - sq;

@@ -34,6 +34,7 @@ struct KParams {
     int32_t tiles_x, tiles_y;      /* 8x8 pixel tiles covering the shard */
     int32_t cost_surf, cost_med;   /* event scheduler weights */
     int32_t chunk;                 /* samples per partial sum (pool kernel) */
+    int32_t taper;                 /* tapered chunk layout (auto mode, vpt_chunks.h) */
 };
 
 #define HIP_OK(expr)                                                                         \
@@ -372,8 +373,10 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
     K.out = d_out;
     if (p->chunk_spp < 0) return vpt_fail(VPT_E_INVALID, "chunk_spp must be >= 0");
     /* auto: 32 samples per work unit (A/B at 1024^2 x 256: chunk 4 / 8 / 16 / 32 / 64 -> 3816 / 3969 /
-     * 4085 / 4153 / 4129 Ms/s); spp <= 32 is then one chunk, i.e. the reference's sequential sum */
+     * 4085 / 4153 / 4129 Ms/s), the last 32 of a pixel tapered (vpt_chunks.h); spp <= 32 is then one
+     * chunk, i.e. the reference's sequential sum.  An explicit chunk_spp gives uniform chunks. */
     K.chunk = p->chunk_spp > 0 ? (p->chunk_spp < p->spp ? p->chunk_spp : p->spp) : (p->spp < 32 ? p->spp : 32);
+    K.taper = p->chunk_spp == 0;
     return VPT_OK;
 }
 
@@ -434,8 +437,9 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         Q.band_stride = K.band_stride;
         Q.band_offset = K.band_offset;
         Q.tiles_x = K.tiles_x;
-        Q.chunk = K.chunk;
-        Q.nch = (K.spp + K.chunk - 1) / K.chunk;
+        Q.lay = vpt_chunks(K.spp, K.chunk, K.taper);
+        Q.nch = Q.lay.n;
+        Q.level_units = (unsigned)K.tiles_x * (unsigned)K.tiles_y * 64u;
         const uint64_t units = (uint64_t)K.tiles_x * (uint64_t)K.tiles_y * 64u * (uint64_t)Q.nch;
         if (units >= 0xFFFFFFFFull) return vpt_fail(VPT_E_INVALID, "too many work units (%llu)", (unsigned long long)units);
         Q.nunits = (unsigned)units;

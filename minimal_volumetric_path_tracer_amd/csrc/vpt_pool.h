@@ -27,6 +27,7 @@
 #ifndef VPT_POOL_H
 #define VPT_POOL_H
 
+#include "vpt_chunks.h"
 #include "vpt_device.h"
 
 namespace vpt {
@@ -48,6 +49,9 @@ namespace vpt {
 #endif
 #ifndef VPT_LOCKFREE
 #define VPT_LOCKFREE 1      /* rings without the ticket lock (ring_entry) */
+#endif
+#ifndef VPT_LATE_UNIT
+#define VPT_LATE_UNIT 0     /* 1: stage-A-only task fields loaded after the S/M body (A/B: 5674 vs 5757 Ms/s, slower) */
 #endif
 #ifndef VPT_PREP_ROUNDS
 #define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s) */
@@ -113,7 +117,9 @@ __device__ __forceinline__ int lds_peek(const int* p)
 struct PoolParams {
     int w, h, spp, rows;
     int band_rows, band_stride, band_offset;
-    int tiles_x, nch, chunk;
+    int tiles_x, nch;
+    vpt_chunk_layout lay;   /* chunks of a pixel's samples (vpt_chunks.h) */
+    unsigned level_units;   /* units per chunk index: 64 pixels x tiles */
     unsigned nunits;
     uint64_t seed;
     double o[3], d[3], cx[3], cy[3];
@@ -121,7 +127,9 @@ struct PoolParams {
     unsigned* queue;
 };
 
-/* work unit -> pixel (8x8 tile order: 64 consecutive units are one tile, one chunk) */
+/* work unit -> pixel and chunk.  Chunk-major: all units of chunk 0 (8x8 tiles in order, 64
+ * consecutive units per tile), then chunk 1, ...; with the tapered layout the last units handed
+ * out are the shortest. */
 struct Unit {
     int x, y, c;
     bool valid;
@@ -130,10 +138,9 @@ struct Unit {
 __device__ __forceinline__ Unit decode_unit(const PoolParams& P, unsigned u)
 {
     Unit r;
-    const unsigned per_tile = 64u * (unsigned)P.nch;
-    const unsigned tile = u / per_tile, rem = u - tile * per_tile;
-    r.c = (int)(rem >> 6);
-    const unsigned p = rem & 63u;
+    const unsigned c = u / P.level_units, rem = u - c * P.level_units;
+    r.c = (int)c;
+    const unsigned tile = rem >> 6, p = rem & 63u;
     r.x = (int)(tile % (unsigned)P.tiles_x) * 8 + (int)(p & 7u);
     const int lr = (int)(tile / (unsigned)P.tiles_x) * 8 + (int)(p >> 3);  /* row within the shard */
     r.valid = r.x < P.w && lr < P.rows;
@@ -168,6 +175,18 @@ struct Task {
     bool in_path, killed;
 };
 
+/* the fields only stage A reads (unit, chunk sum, sample counter): loaded right before it */
+__device__ __forceinline__ void load_task_unit(const TaskPool& sh, int s, Task& t)
+{
+    t.acc = mk(sh.f[F_AX][s], sh.f[F_AY][s], sh.f[F_AZ][s]);
+    t.key = (uint64_t)__double_as_longlong(sh.f[F_KEY][s]);
+    t.pix = sh.pix[s];
+    t.c1 = sh.c1[s];
+    const uint32_t sm = sh.samp[s];
+    t.i = sm & 0x7FFFFFFFu;
+    t.in_path = (sm >> 31) != 0;
+}
+
 __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bool full)
 {
     t.p.o = mk(sh.f[F_OX][s], sh.f[F_OY][s], sh.f[F_OZ][s]);
@@ -182,15 +201,7 @@ __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bo
     t.e.src = (int)((ev >> 24) & 0x7Fu);
     t.killed = (ev >> 31) != 0;
     t.X = sh.X[s];
-    if (full) {
-        t.acc = mk(sh.f[F_AX][s], sh.f[F_AY][s], sh.f[F_AZ][s]);
-        t.key = (uint64_t)__double_as_longlong(sh.f[F_KEY][s]);
-        t.pix = sh.pix[s];
-        t.c1 = sh.c1[s];
-        const uint32_t sm = sh.samp[s];
-        t.i = sm & 0x7FFFFFFFu;
-        t.in_path = (sm >> 31) != 0;
-    }
+    if (full) load_task_unit(sh, s, t);
 }
 
 __device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, bool full)
@@ -220,7 +231,7 @@ __device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t
     const int fr = P.h - 1 - y;
     const int k = fr / P.band_rows, rr = fr - k * P.band_rows;
     const int lr = ((k - P.band_offset) / P.band_stride) * P.band_rows + rr;
-    const int c = (int)((t.c1 - 1u) / (unsigned)P.chunk);
+    const int c = vpt_chunk_of_end(&P.lay, (int)t.c1);
     const size_t o = (((size_t)lr * (size_t)P.w + (size_t)x) * (size_t)P.nch + (size_t)c) * 3;
     P.partials[o] = t.acc.x;
     P.partials[o + 1] = t.acc.y;
@@ -290,8 +301,10 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                     if (uu.valid) {  /* (an invalid unit -- a tile's padding -- is dropped) */
                         t.pix = (unsigned)uu.x | ((unsigned)uu.y << 16);
                         t.key = vpt_stream_key(P.seed, (uint64_t)(P.h - 1 - uu.y) * (uint64_t)P.w + (uint64_t)uu.x);
-                        t.i = (unsigned)(uu.c * P.chunk);
-                        t.c1 = (unsigned)min((uu.c + 1) * P.chunk, P.spp);
+                        int s0, s1;
+                        vpt_chunk_range(&P.lay, uu.c, &s0, &s1);
+                        t.i = (unsigned)s0;
+                        t.c1 = (unsigned)s1;
                         t.in_path = false;
                         t.acc = mk(0, 0, 0);
                     }
@@ -635,7 +648,7 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
             if (active) store_task(sh, slot, t, true);
         } else {
             if (active) {
-                load_task(sh, slot, t, VPT_FUSE_A != 0);
+                load_task(sh, slot, t, VPT_FUSE_A != 0 && !VPT_LATE_UNIT);
                 smp.X = t.X;
                 /* surface rings are keyed by material: diffuse (R_S, R_S+1), metal (R_S+2), other */
                 /* and by light kind: sphere light (R_S, R_M), point light (R_S + 1, R_M + 1) */
@@ -660,6 +673,7 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
             /* every task leaving S/M goes to stage A: the same wave runs it on the same lanes
              * right away, instead of storing the batch, returning it to ring A under the lock and
              * loading it again in another wave */
+            if (VPT_LATE_UNIT && active) load_task_unit(sh, slot, t);  /* not live across S/M */
             next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
             if (active) store_task(sh, slot, t, true);
 #else

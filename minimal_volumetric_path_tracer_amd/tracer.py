@@ -77,7 +77,7 @@ class RenderConfig:
     band_rows: int = 0          # 0 = whole image
     band_stride: int = 1
     band_offset: int = 0
-    chunk_spp: int = 0          # 0 = auto (min(spp, 32)); 1 or >= spp = the reference's sequential sum
+    chunk_spp: int = 0          # 0 = auto (min(spp, 32), the last 64 samples tapered); 1 or >= spp = the reference's sequential sum
 
     def params(self) -> _lib.vpt_params:
         p = _lib.vpt_params()

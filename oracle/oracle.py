@@ -87,6 +87,8 @@ class Oracle:
         L.orc_render.argtypes = [_I, _I, _I, POINTER(Medium), _U, _I, _I, _P, _I, POINTER(Counters)]
         L.orc_render_chunked.restype = None
         L.orc_render_chunked.argtypes = [_I, _I, _I, _I, POINTER(Medium), _U, _I, _I, _P, _I, POINTER(Counters)]
+        L.orc_render_layout.restype = None
+        L.orc_render_layout.argtypes = [_I, _I, _I, _I, _I, POINTER(Medium), _U, _I, _I, _P, _I, POINTER(Counters)]
         L.orc_write_ppm.restype, L.orc_write_ppm.argtypes = _I, [ctypes.c_char_p, _P, _I, _I]
         L.orc_stream_state_c.restype, L.orc_stream_state_c.argtypes = _U, [_U, _U, _U]
         L.orc_is_portable_math.restype = _I
@@ -119,14 +121,17 @@ class Oracle:
     def render(self, w, h, spp, estimator=0, sigma_a=0.001, sigma_s=0.009, hg_g=0.0, max_depth=0, seed=0x5EED0001,
                y0=0, y1=None, threads=0, counters=False, chunk=None):
         """main()'s pixel loop over camera rows [y0, y1); returns (h, w, 3) float64 in file order.
-        chunk: samples per partial sum (None = the GPU's default, min(spp, 32); spp = reference order)."""
+        chunk: samples per partial sum in uniform chunks (spp = the reference's order); None = the
+        GPU's default (vpt_params.chunk_spp == 0): chunks of min(spp, 32), the last 32 tapered
+        (csrc/vpt_chunks.h)."""
         m = Medium(sigma_a, sigma_s, hg_g, max_depth, estimator)
         out = np.zeros((h, w, 3))
         c = Counters()
-        if chunk is None:
-            chunk = default_chunk(spp)
-        self.L.orc_render_chunked(w, h, spp, chunk, byref(m), seed, y0, h if y1 is None else y1, out.ctypes.data,
-                                  threads, byref(c))
+        taper = 0
+        if chunk is None or chunk == 0:
+            chunk, taper = default_chunk(spp), 1
+        self.L.orc_render_layout(w, h, spp, chunk, taper, byref(m), seed, y0, h if y1 is None else y1,
+                                 out.ctypes.data, threads, byref(c))
         return (out, c) if counters else out
 
     def math(self, fn: int, x: np.ndarray, y=None) -> np.ndarray:

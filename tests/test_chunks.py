@@ -1,0 +1,61 @@
+"""Chunk layout of a pixel's samples (csrc/vpt_chunks.h, shared by the kernels and the oracle):
+uniform chunks, and the tapered auto layout whose short last chunks end a launch without a long
+sequential tail.  CPU only (through the oracle library, which compiles the same header)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+
+
+def layout(orc, spp, chunk, taper):
+    buf = (ctypes.c_int * 8200)()
+    n = orc.L.orc_chunk_layout(spp, chunk, taper, buf, 8200)
+    assert n > 0, n  # -2 would mean vpt_chunk_of_end is not the inverse of vpt_chunk_range
+    return list(buf[: n + 1])
+
+
+@pytest.fixture(scope="module")
+def orc():
+    o = Oracle(portable=True)
+    o.L.orc_chunk_layout.restype = ctypes.c_int
+    o.L.orc_chunk_layout.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    return o
+
+
+def test_tapered_layout_bench_config(orc):
+    # 1024^2 x 256 (BASELINE configs[1]): 6 chunks of 32, then the last 64 samples as 22, 14, 10, 6, 4, 3, 2, 1, 1, 1
+    assert layout(orc, 256, 32, 1) == [0, 32, 64, 96, 128, 160, 192, 214, 228, 238, 244, 248, 251, 253, 254, 255, 256]
+    assert layout(orc, 256, 32, 0) == list(range(0, 257, 32))
+
+
+@pytest.mark.parametrize("spp", [1, 2, 5, 16, 31, 32, 33, 40, 63, 64, 70, 100, 1024, 4096])
+@pytest.mark.parametrize("chunk,taper", [(32, 1), (32, 0), (7, 0), (7, 1), (1, 0), (1, 1)])
+def test_layout_partitions_samples(orc, spp, chunk, taper):
+    st = layout(orc, spp, chunk, taper)
+    sizes = np.diff(st)
+    assert st[0] == 0 and st[-1] == spp and (sizes > 0).all()
+    C = min(chunk, spp)
+    if not taper or spp <= C:
+        assert (sizes[:-1] == C).all() and sizes[-1] <= C
+    else:
+        R = min(spp, 2 * C)
+        head = spp - R
+        nh = -(-head // C)
+        assert st[nh] == head and (sizes[: max(nh - 1, 0)] == C).all()
+        tail = sizes[nh:]
+        assert tail.sum() == R and (np.diff(tail) <= 0).all() and tail[-1] == 1
+        # the work behind every chunk is at least twice the chunk (latency cover, vpt_chunks.h)
+        behind = np.cumsum(sizes[::-1])[::-1] - sizes
+        assert (behind[nh:] >= 2 * tail - 2).all()  # (ceil rounding: within two samples)
+
+
+def test_tapered_render_is_a_reordered_sum(orc):
+    """same samples, only the summation order differs from the reference's sequential sum"""
+    orc.set_scene(__import__("minimal_volumetric_path_tracer_amd").default_scene())
+    a = orc.render(8, 6, 40, 0, seed=9, threads=2)              # auto: tapered chunks of 32
+    b = orc.render(8, 6, 40, 0, seed=9, threads=2, chunk=40)    # one chunk: the reference's order
+    c = orc.render(8, 6, 40, 0, seed=9, threads=2, chunk=32)    # uniform chunks
+    assert np.allclose(a, b, rtol=1e-12, atol=1e-14) and np.allclose(a, c, rtol=1e-12, atol=1e-14)
+    assert not np.array_equal(a, c) or not np.array_equal(a, b)  # the layouts do differ somewhere

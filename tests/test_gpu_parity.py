@@ -133,12 +133,13 @@ def test_render_vs_oracle_bitwise(gpu_tracer, orc_vm, est):
 
 @pytest.mark.parametrize("spp,chunk", [(40, 0), (40, 7), (40, 40), (40, 1), (33, 0), (70, 0)])
 def test_chunked_sums_vs_oracle(gpu_tracer, orc_vm, spp, chunk):
-    """samples summed in chunks (vpt_params.chunk_spp; auto = min(spp, 32)); chunk 1 or spp = reference order."""
+    """samples summed in chunks (vpt_params.chunk_spp; auto = chunks of min(spp, 32), the last 32 tapered,
+    csrc/vpt_chunks.h); chunk 1 or spp = reference order."""
     sc = SCENES["default"]()
     gpu_tracer.set_scene(sc)
     orc_vm.set_scene(sc)
     g = gpu_tracer.render(width=20, height=12, spp=spp, chunk_spp=chunk, seed=4, fp64=True)
-    eff = chunk if chunk > 0 else min(spp, 32)
+    eff = chunk if chunk > 0 else None  # None: the auto (tapered) layout
     o = orc_vm.render(20, 12, spp, 0, seed=4, chunk=eff, threads=4)
     assert bitwise_equal(g, o).all()
     if chunk in (1, spp):
@@ -370,6 +371,6 @@ def test_pool_work_handout_vs_oracle(gpu_tracer, orc_vm, w, h, spp, chunk):
     gpu_tracer.set_scene(sc)
     orc_vm.set_scene(sc)
     g = gpu_tracer.render(width=w, height=h, spp=spp, chunk_spp=chunk, seed=21, fp64=True)
-    eff = chunk if chunk > 0 else min(spp, 32)
+    eff = chunk if chunk > 0 else None  # None: the auto (tapered) layout
     o = orc_vm.render(w, h, spp, 0, seed=21, chunk=eff, threads=4)
     assert g.shape == o.shape and bitwise_equal(g, o).all()
