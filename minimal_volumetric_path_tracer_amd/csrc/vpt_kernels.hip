@@ -468,8 +468,9 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         HIP_OK(hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned), stream));
         unsigned long long* stats = nullptr;
         if (env_int("VPT_POOL_STATS", 0)) {  /* debug: scheduler statistics, vpt_debug_pool_stats */
-            if (!g_pool_stats) HIP_OK(hipMalloc((void**)&g_pool_stats, NSTATS * sizeof(unsigned long long)));
-            HIP_OK(hipMemsetAsync(g_pool_stats, 0, NSTATS * sizeof(unsigned long long), stream));
+            if (!g_pool_stats) HIP_OK(hipMalloc((void**)&g_pool_stats, (TL0 + 3 * TL_MAXWG) * sizeof(unsigned long long)));
+            HIP_OK(hipMemsetAsync(g_pool_stats, 0, TL0 * sizeof(unsigned long long), stream));
+            HIP_OK(hipMemsetAsync(g_pool_stats + TL0, 0xFF, 3 * TL_MAXWG * sizeof(unsigned long long), stream));
             stats = g_pool_stats;
         }
         pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(Q, m, S, K.counters, stats);
@@ -745,5 +746,14 @@ extern "C" int vpt_debug_pool_stats(unsigned long long* out)
     if (!g_pool_stats || !out) return VPT_E_INVALID;
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(out, g_pool_stats, NSTATS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return VPT_OK;
+}
+
+/* debug: the per-workgroup timeline of the last VPT_POOL_STATS launch (vpt_pool.h TL0), 3 x TL_MAXWG */
+extern "C" int vpt_debug_pool_timeline(unsigned long long* out)
+{
+    if (!g_pool_stats || !out) return VPT_E_INVALID;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(out, g_pool_stats + TL0, 3 * TL_MAXWG * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return VPT_OK;
 }

@@ -68,6 +68,14 @@ constexpr int URING = 256, UREFILL = 128;  /* work-unit ring: one global queue a
  * per ring, [14] idle polls, [15] ticket waits, [16-19] cycles in stage A/S/M/scheduling, [20]
  * stage-A preparation rounds, [21] samples started, [22] cycles preparing, [23] cycles in decide */
 constexpr int NSTATS = 24;
+/* debug timeline (s_memrealtime, 100 MHz) after the counters: per workgroup b, stats[TL0 + 3b + k] =
+ * min over its waves of k=0 start, k=1 first sight of the exhausted work queue, k=2 ~exit time */
+constexpr int TL0 = 32, TL_MAXWG = 4096;
+__device__ __forceinline__ void dbg_tl(unsigned long long* stats, int k, bool inv)
+{
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x < (unsigned)TL_MAXWG) atomicMin(&stats[TL0 + 3 * blockIdx.x + k], inv ? ~t : t);
+}
 struct ADbg {
     unsigned long long rounds, samples, c_prep, c_decide;
 };
@@ -408,6 +416,8 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
     const bool dbg = VPT_POOL_DEBUG && stats != nullptr;  /* compiled out of production builds */
     const bool dbga = VPT_POOL_DEBUG == 1 && dbg;          /* stage-A internals (VPT_POOL_DEBUG=2: top level only) */
     unsigned long long tclk = dbg_clock(dbg);
+    bool seen_exh = false;
+    if (dbg && tid == 0) dbg_tl(stats, 0, false);
     while (true) {
 #if VPT_LOCKFREE
         /* ---- scheduling without a lock (ring_entry): reserve, publish, claim ---- */
@@ -435,6 +445,10 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
          * wave at a time, claimed by a flag */
         {
             const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+            if (dbg && !seen_exh && __builtin_amdgcn_readlane(v, C_EXH)) {
+                seen_exh = true;
+                if (lane == 0) dbg_tl(stats, 1, false);
+            }
             if (!__builtin_amdgcn_readlane(v, C_EXH) && !__builtin_amdgcn_readlane(v, C_RFL) &&
                 __builtin_amdgcn_readlane(v, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL) {
                 int own = 0;
@@ -694,6 +708,7 @@ __global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, M
         atomicAdd(&counters[1], (unsigned long long)smp.cnt.iterations);
     }
     if (dbg) {
+        if (lane == 0) dbg_tl(stats, 2, true);
         atomicAdd(&stats[21], D.samples);
         if (lane == 0) {
             atomicAdd(&stats[14], st_idle);
