@@ -98,10 +98,13 @@ typedef struct vpt_params {
      * and writes them compactly, in increasing file-row order.  Whole image: band_rows = height,
      * band_stride = 1, band_offset = 0 (vpt_default_params). */
     int32_t band_rows, band_stride, band_offset;
-    /* Samples per partial sum (build extension; 0 = auto = min(spp, 32)).  A pixel's samples are
-     * summed sequentially inside a chunk exactly as the reference sums a pixel (src/rt.cpp:794),
-     * and the chunk sums are then added in chunk order; chunk_spp == 1 or >= spp is the
-     * reference's own sequential order.  Chunks are the GPU's unit of work. */
+    /* Samples per partial sum (build extension).  A pixel's samples are summed sequentially inside
+     * a chunk exactly as the reference sums a pixel (src/rt.cpp:794), and the chunk sums are then
+     * added in chunk order; chunk_spp == 1 or >= spp is the reference's own sequential order.
+     * Chunks are the GPU's unit of work.  chunk_spp > 0: uniform chunks of chunk_spp samples;
+     * 0 = auto: chunks of min(spp, 32), the last 64 samples in shrinking chunks (22, 14, 10, ...,
+     * 1; layout in csrc/vpt_chunks.h) so that a launch ends on short units.  spp <= 32 is one
+     * chunk either way. */
     int32_t chunk_spp;
 } vpt_params;
 
