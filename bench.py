@@ -49,6 +49,36 @@ CONFIGS = {
 }
 
 
+def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 4, band: int = 16) -> dict:
+    """The oracle restatement (oracle/liboracle_vm.so: per-sample streams, the kernel's portable
+    libm) timed on `bands` bands of `band` camera rows of the bench image, same seed and chunk
+    layout, and compared with the GPU image on those rows: per-channel RMSE of the linear float32
+    framebuffer (the metric's "per-channel RMSE vs CPU"; the bar is bit-exact, RMSE 0)."""
+    from oracle.oracle import Oracle  # cpu_baseline leg only
+
+    H, W, SPP = c["height"], c["width"], c["spp"]
+    o = Oracle(portable=True)
+    o.set_scene(vpt.default_scene())
+    from minimal_volumetric_path_tracer_amd.tracer import ESTIMATORS
+
+    est = ESTIMATORS[c["estimator"]]
+    se, n, el = np.zeros(3), 0, 0.0
+    for k in range(bands):
+        y0 = (H - band) * k // max(bands - 1, 1)
+        t = time.time()
+        ref = o.render(W, H, SPP, est, sigma_a=c["sigma_a"], sigma_s=c["sigma_s"], hg_g=c.get("hg_g", 0.0),
+                       max_depth=c.get("max_depth", 0), seed=0x5EED0001, y0=y0, y1=y0 + band, threads=threads)
+        el += time.time() - t
+        rows = slice(H - y0 - band, H - y0)  # file rows of camera rows [y0, y0 + band)
+        d = img[rows].astype(np.float64) - ref[rows].astype(np.float32).astype(np.float64)
+        se += (d * d).reshape(-1, 3).sum(0)
+        n += band * W
+    return {"value": bands * band * W * SPP / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle restatement (per-sample erand48 streams, portable libm), {bands} bands of {band} rows "
+                      f"x {W} x {SPP} spp of the bench image, {threads} threads, {el:.1f}s",
+            "rmse_vs_gpu_per_channel": [float(x) for x in np.sqrt(se / n)]}
+
+
 def cpu_baseline(threads: int) -> dict:
     """The reference program itself (oracle/_ref/rt, built from /root/reference's sources by
     oracle/Makefile) on this host's cores: `rt 32` = 1024x768x32 (25 M samples, ~13 s) with its racy
@@ -275,6 +305,8 @@ def main() -> None:
         if world == 1 and not args.no_cpu:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
             res["cpu_baseline"] = cpu_baseline(threads)
+            # the per-thread-RNG flavour + the per-channel RMSE of sampled rows vs the GPU image
+            res["cpu_baseline"]["port_per_sample_rng"] = cpu_port_check(img, c, threads)
         print(json.dumps(res))
     for t in tracers:
         t.close()
