@@ -49,7 +49,7 @@ CONFIGS = {
 }
 
 
-def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 4, band: int = 16) -> dict:
+def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 12, band: int = 16) -> dict:
     """The oracle restatement (oracle/liboracle_vm.so: per-sample streams, the kernel's portable
     libm) timed on `bands` bands of `band` camera rows of the bench image, same seed and chunk
     layout, and compared with the GPU image on those rows: per-channel RMSE of the linear float32
