@@ -66,9 +66,13 @@ typedef enum {
     VPT_MIS_EQUIANGULAR = 1,       /* MISVPTTracerRecursive, vptShadeMethods.h:1345 */
     VPT_EXPLICIT_FREE = 2,         /* explicitVPTracerRecursiveFree, vptShadeMethods.h:1153 */
     VPT_IMPLICIT_FREE = 3,         /* implicitVPTracerRecursiveFree, vptShadeMethods.h:940 */
-    VPT_EXPLICIT_EQUIANGULAR = 4   /* explicitVPTracerRecursive, vptShadeMethods.h:1014 */
+    VPT_EXPLICIT_EQUIANGULAR = 4,  /* explicitVPTracerRecursive, vptShadeMethods.h:1014 */
+    VPT_SURFACE_PT = 5             /* iterativePathTracer, shadeMethods.h:104: surface-only path tracing (the
+                                    * commented alternative at src/rt.cpp:793); sigma_a, sigma_s, hg_g and
+                                    * max_depth are ignored; renders sum each pixel's samples in the
+                                    * reference's sequential order (chunk_spp ignored) */
 } vpt_estimator;
-#define VPT_NUM_ESTIMATORS 5
+#define VPT_NUM_ESTIMATORS 6
 
 typedef enum {
     VPT_FB_F32 = 0,            /* framebuffer: 3 x float per pixel */

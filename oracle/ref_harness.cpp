@@ -30,6 +30,7 @@
 #include "volumetricBasicFunctions.h"
 #include "vptSamplingFunctions.h"
 #include "vptShadeMethods.h"
+#include "shadeMethods.h"
 
 extern "C" {
 #include "oracle_rng.h"
@@ -103,7 +104,8 @@ void ref_set_scene(const void* in, int n)
  *   1 MISVPTTracerRecursive          vptShadeMethods.h:1345
  *   2 explicitVPTracerRecursiveFree  vptShadeMethods.h:1153
  *   3 implicitVPTracerRecursiveFree  vptShadeMethods.h:938
- *   4 explicitVPTracerRecursive      vptShadeMethods.h:1014 */
+ *   4 explicitVPTracerRecursive      vptShadeMethods.h:1014
+ *   5 iterativePathTracer            shadeMethods.h:104 (surface only: sa, ss unused) */
 static Color run_estimator(int estimator, const Ray& r, double sa, double ss)
 {
     switch (estimator) {
@@ -111,7 +113,8 @@ static Color run_estimator(int estimator, const Ray& r, double sa, double ss)
     case 1: return MISVPTTracerRecursive(r, sa, ss, 0);
     case 2: return explicitVPTracerRecursiveFree(r, sa, ss, 0);
     case 3: return implicitVPTracerRecursiveFree(r, sa, ss);
-    default: return explicitVPTracerRecursive(r, sa, ss, 0);
+    case 4: return explicitVPTracerRecursive(r, sa, ss, 0);
+    default: return iterativePathTracer(r);
     }
 }
 

@@ -28,7 +28,7 @@ typedef struct {
     double sigma_a, sigma_s;  /* src/rt.cpp:794 */
     double hg_g;              /* extension: 0 = reference isotropic phase */
     int32_t max_depth;        /* extension: 0 = unbounded (reference) */
-    int32_t estimator;        /* 0 = iterativeVPTracerFree, 1 = MISVPTTracerRecursive */
+    int32_t estimator;        /* include/vpt.h vpt_estimator: 0 iterativeVPTracerFree, 1 MISVPTTracerRecursive, ..., 5 iterativePathTracer */
 } orc_medium;
 
 typedef struct {           /* work counters (counting mode) */

@@ -50,6 +50,12 @@ def samples_alt():
 
 
 @pytest.fixture(scope="session")
+def samples_e5():
+    """iterativePathTracer (estimator 5) on the test + alternate scenes (make_golden.py --surface-pt)"""
+    return dict(np.load(os.path.join(GOLDEN, "samples_e5.npz")))
+
+
+@pytest.fixture(scope="session")
 def prims():
     return dict(np.load(os.path.join(GOLDEN, "primitives.npz")))
 

@@ -257,12 +257,33 @@ def alt_scenes():
     print("wrote", os.path.join(HERE, "samples_alt.npz"))
 
 
+def surface_pt():
+    """iterativePathTracer (include/shadeMethods.h:104, surface only; estimator 5) on every test
+    scene and alternate scene -> samples_e5.npz.  Own RNG seed: the other fixtures stay byte-identical."""
+    ref = Reference()
+    rng = np.random.default_rng(20261017)
+    bundle = {}
+    for name, mk in {**EST_SCENES, **ALT_SCENES}.items():
+        sc = mk()
+        ref.set_scene(sc)
+        bundle[f"{name}__scene"] = sc.view(np.uint8)
+        ps = per_sample(ref, 5, 256, rng)
+        for k, v in ps.items():
+            bundle[f"{name}__e5__{k}"] = v
+        bundle[f"{name}__e5__fb24x24x4"] = ref.render(24, 24, 4, 5, seed=SEED)
+    np.savez_compressed(os.path.join(HERE, "samples_e5.npz"), **bundle)
+    print("wrote", os.path.join(HERE, "samples_e5.npz"))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["--estimators-234"]:
         estimators_234()
     elif sys.argv[1:] == ["--alt-scenes"]:
         alt_scenes()
+    elif sys.argv[1:] == ["--surface-pt"]:
+        surface_pt()
     else:
         main()
         estimators_234()
         alt_scenes()
+        surface_pt()

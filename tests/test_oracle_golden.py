@@ -251,3 +251,26 @@ def test_alt_scenes_vs_reference(samples_alt, orc, scene, est):
         assert bitwise_equal(out, samples_alt[k + "fb24x24x4"]).all()
     else:
         _close_nan_aware(out, samples_alt[k + "fb24x24x4"])
+
+
+# ---- iterativePathTracer (include/shadeMethods.h:104): surface-only estimator 5
+from scenes import EST_SCENES  # noqa: E402
+
+E5_SCENES = list(EST_SCENES) + list(ALT_SCENES)
+
+
+@pytest.mark.parametrize("scene", E5_SCENES)
+def test_surface_pt_vs_reference(samples_e5, orc, scene):
+    """same draws and the same bits as the reference (MIS = MISv2 without the transmitance factor,
+    BDSF = bdsf, pLight over every r == 0 sphere), per sample and on a 24x24x4 framebuffer"""
+    orc.set_scene(samples_e5[f"{scene}__scene"])
+    k = f"{scene}__e5__"
+    L, st = orc.trace(5, samples_e5[k + "ray"], samples_e5[k + "state1"])
+    assert np.array_equal(st, samples_e5[k + "state2"]), "random draws consumed differ"
+    assert bitwise_equal(L, samples_e5[k + "L"]).all()
+    out = orc.render(24, 24, 4, 5, seed=SEED, threads=2, chunk=4)  # chunk = spp: the reference's order
+    assert bitwise_equal(out, samples_e5[k + "fb24x24x4"]).all()
+    # the fixture exercises the path -- except where the reference's own tests make the image black:
+    # no emitter, or (alt_area_light) a light with radiance.x == 0, which iterativePathTracer and MIS
+    # never treat as a light (include/shadeMethods.h:122, include/misSamplingFunctions.h:29)
+    assert (samples_e5[k + "L"] != 0).any() == (scene not in ("no_emitter", "alt_area_light"))
