@@ -587,8 +587,9 @@ VPT_DEV double power_heuristic(double f, double g)
     return f2 / (f2 + g2);
 }
 
-/* MISv2, include/misSamplingFunctions.h:96-170 */
-template <bool COUNT, int MK = -1>
+/* MISv2, include/misSamplingFunctions.h:96-170 (TR = true), and MIS, :19-91 (TR = false): the same
+ * function without the transmitance factor on the light samples (:29 vs :106) */
+template <bool COUNT, int MK = -1, bool TR = true>
 VPT_DEV dv3 mis_v2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray, double alpha,
                    double sigma_t)
 {
@@ -601,7 +602,7 @@ VPT_DEV dv3 mis_v2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj,
     for (int k = 0; k < S->n_mis; ++k) {  /* spheres with r > 0 && radiance.x > 0, in index order */
         const int light = S->mis_light[k];
         dv3 f = light_sample_sa(S, smp, light, x, obj, omat, n, wray, wiLight, cmax, alpha);
-        f = scl(f, transmitance(x, sph_p(S, light), sigma_t));
+        if (TR) f = scl(f, transmitance(x, sph_p(S, light), sigma_t));
         fpdf = solid_angle_prob(cmax);
         if (omat == 0) {
             gpdf = hemi_cosine_prob(dot(n, wiLight));
@@ -1166,25 +1167,74 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
     p.depth++;
 }
 
+/* iterativePathTracer, include/shadeMethods.h:104-163 (estimator 5): surface-only path tracing.
+ * Per iteration: nearest hit or end (:117-119); a light (radiance.x > 0) seen by the camera ray
+ * returns its radiance, a later one ends the path (:122-125); pLight for every r == 0 sphere in
+ * index order, then MIS (:133-141, Ld = term + Ld); the roulette draw, which drops this vertex's
+ * Ld (:143-147); the BSDF continuation (:149, BDSF == bdsf), unnormalised (:151-153).  prob and wi
+ * live across iterations as in the reference (a material-3 hit leaves them unchanged). */
+template <bool COUNT>
+__device__ static dv3 trace_surface_pt(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d)
+{
+    dv3 Accum = mk(0, 0, 0), fs = mk(1, 1, 1), Ld = mk(0, 0, 0), wi = mk(0, 0, 0);
+    int bounces = 0;
+    double factor = 1;
+    const double q = 0.4;
+    const double continueprob = 1.0 - q;
+    double prob = 0;
+    const int n = S->n;
+    while (true) {
+        if (COUNT) smp.cnt.iterations++;
+        double t;
+        int id = 0;
+        if (!scene_intersect(S, smp, o, d, t, id, false)) break;
+        if (S->sph[id].radiance[0] > 0) {
+            if (bounces < 1) return sph_rad(S, id);
+            break;
+        }
+        const dv3 x = add(o, scl(d, t));
+        const dv3 nx = nrm(sub(x, sph_p(S, id)));
+        const double alpha = S->sph[id].alpha;
+        for (int l = 0; l < n; ++l)  /* wave-uniform: scalar loads of the scene */
+            if (S->sph[l].r == 0) Ld = add(p_light<COUNT>(S, smp, id, x, nx, d, l, alpha), Ld);
+        Ld = add(mis_v2<COUNT, -1, false>(S, smp, id, x, nx, d, alpha, 0.0), Ld);
+        if (smp.next() < q) break;
+        const dv3 fs1 = bdsf<COUNT>(S, smp, wi, d, nx, prob, id);
+        o = x;
+        d = wi;
+        const double cosine = dot(nx, wi);
+        Accum = add(Accum, scl(mul(fs, Ld), factor));
+        fs = mul(fs, fs1);
+        factor = factor * cosine * (1 / (prob * continueprob));
+        bounces++;
+        Ld = mk(0, 0, 0);
+    }
+    return Accum;
+}
+
 /* One camera sample, sequentially (the reference's per-sample call; used by vpt_trace_batch). */
 template <int EST, bool COUNT>
 __device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, const Medium& m)
 {
-    Path p;
-    p.o = o;
-    p.d = d;
-    p.beta = mk(1, 1, 1);
-    p.L = mk(0, 0, 0);
-    p.depth = 0;
-    Event e;
-    e.pdf = 0;
-    while (continue_path(smp, p, m)) {
-        int ev = decide<EST>(S, smp, p, e, m);
-        if (ev == EV_END) break;
-        if (ev == EV_SURF) surface_event<EST>(S, smp, p, e, m);
-        else medium_event<EST>(S, smp, p, e, m);
+    if constexpr (EST == 5) {
+        return trace_surface_pt<COUNT>(S, smp, o, d);
+    } else {
+        Path p;
+        p.o = o;
+        p.d = d;
+        p.beta = mk(1, 1, 1);
+        p.L = mk(0, 0, 0);
+        p.depth = 0;
+        Event e;
+        e.pdf = 0;
+        while (continue_path(smp, p, m)) {
+            int ev = decide<EST>(S, smp, p, e, m);
+            if (ev == EV_END) break;
+            if (ev == EV_SURF) surface_event<EST>(S, smp, p, e, m);
+            else medium_event<EST>(S, smp, p, e, m);
+        }
+        return p.L;
     }
-    return p.L;
 }
 
 }  // namespace vpt

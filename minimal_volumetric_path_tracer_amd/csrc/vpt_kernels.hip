@@ -414,7 +414,12 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         HIP_OK(hipGetLastError());
         return VPT_OK;
     }
-    if constexpr (!COUNT) return launch_pool<EST, FB>(ctx, K, stream);
+    if constexpr (!COUNT && EST != 5) return launch_pool<EST, FB>(ctx, K, stream);
+    if constexpr (EST == 5) {  /* iterativePathTracer: one lane per pixel, samples summed in order */
+        dim3 grid((unsigned)((K.w + 15) / 16), (unsigned)((K.shard_rows + 15) / 16));
+        render_kernel_simple<EST, COUNT, FB><<<grid, dim3(256), 0, stream>>>(K, S);
+        HIP_OK(hipGetLastError());
+    }
     return VPT_OK;
 }
 
@@ -520,6 +525,7 @@ static int launch_render(vpt_context* ctx, KParams K, hipStream_t stream)
         VPT_LAUNCH_EST(2)
         VPT_LAUNCH_EST(3)
         VPT_LAUNCH_EST(4)
+        VPT_LAUNCH_EST(5)
     }
 #undef VPT_LAUNCH_EST
     return vpt_fail(VPT_E_INVALID, "unknown estimator %d", K.est);
@@ -698,7 +704,8 @@ int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, 
         case 1: trace_batch_kernel<1><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         case 2: trace_batch_kernel<2><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         case 3: trace_batch_kernel<3><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
-        default: trace_batch_kernel<4><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        case 4: trace_batch_kernel<4><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        default: trace_batch_kernel<5><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         }
         e = hipGetLastError();
     }

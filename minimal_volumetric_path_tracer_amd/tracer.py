@@ -24,11 +24,11 @@ import numpy as np
 
 from . import _lib
 from ._lib import (EXPLICIT_EQUIANGULAR, EXPLICIT_FREE, FB_F32, FB_F64, FREE_FLIGHT, IMPLICIT_FREE, MIS_EQUIANGULAR,
-                   RAY_DTYPE, SPHERE_DTYPE, check, lib)
+                   RAY_DTYPE, SPHERE_DTYPE, SURFACE_PT, check, lib)
 
 ESTIMATORS = {"ff": FREE_FLIGHT, "free_flight": FREE_FLIGHT, "mis": MIS_EQUIANGULAR, "mis_equiangular": MIS_EQUIANGULAR,
               "explicit_free": EXPLICIT_FREE, "implicit_free": IMPLICIT_FREE, "explicit": EXPLICIT_EQUIANGULAR,
-              "explicit_equiangular": EXPLICIT_EQUIANGULAR}
+              "explicit_equiangular": EXPLICIT_EQUIANGULAR, "surface_pt": SURFACE_PT, "path_tracer": SURFACE_PT}
 
 
 def Sphere(r, p, c=(0, 0, 0), radiance=(0, 0, 0), material=0, eta=(0, 0, 0), kappa=(0, 0, 0), alpha=0.0) -> np.ndarray:
@@ -182,6 +182,10 @@ class Tracer:
     def explicitVPTracerRecursive(self, rays, states, sigma_a=0.001, sigma_s=0.009, **kw):
         """Batched include/vptShadeMethods.h:1014 (depth 0)."""
         return self.trace("explicit", rays, states, sigma_a, sigma_s, **kw)
+
+    def iterativePathTracer(self, rays, states):
+        """Batched include/shadeMethods.h:104 (surface only: no medium arguments)."""
+        return self.trace("surface_pt", rays, states)
 
     def math_probe(self, fn: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float64)

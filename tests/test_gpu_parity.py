@@ -374,3 +374,79 @@ def test_pool_work_handout_vs_oracle(gpu_tracer, orc_vm, w, h, spp, chunk):
     eff = chunk if chunk > 0 else None  # None: the auto (tapered) layout
     o = orc_vm.render(w, h, spp, 0, seed=21, chunk=eff, threads=4)
     assert g.shape == o.shape and bitwise_equal(g, o).all()
+
+
+# ---------------------------------------------------------------- estimator 5: iterativePathTracer
+E5_SCENES = list(EST_SCENES) + list(ALT_SCENES)
+
+
+def _e5_scene(name):
+    return (EST_SCENES.get(name) or ALT_SCENES[name])()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", E5_SCENES)
+def test_trace_batch_vs_oracle_bitwise_e5(gpu_tracer, orc_vm, samples_e5, scene):
+    """include/shadeMethods.h:104 per sample: same draws, same bits as the oracle"""
+    sc = samples_e5[f"{scene}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    k = f"{scene}__e5__"
+    rays, st = samples_e5[k + "ray"], samples_e5[k + "state1"]
+    L, s = gpu_tracer.iterativePathTracer(_rays(rays), st)
+    Lo, so = orc_vm.trace(5, rays, st)
+    assert np.array_equal(s, so)
+    same = bitwise_equal(L, Lo)
+    assert same.all(), f"{(~same.all(1)).sum()} of {len(L)} samples differ"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["default", "dielectric", "alt_metal_walls"])
+def test_trace_batch_vs_reference_e5(gpu_tracer, samples_e5, scene):
+    """against the reference's own per-sample values (the statistics bar of the other estimators:
+    the build's portable libm re-rolls a few rounding-dependent branches)"""
+    sc = samples_e5[f"{scene}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    k = f"{scene}__e5__"
+    L, s = gpu_tracer.trace(5, _rays(samples_e5[k + "ray"]), samples_e5[k + "state1"])
+    ref = samples_e5[k + "L"]
+    assert (s == samples_e5[k + "state2"]).mean() >= 0.97
+    close = bitwise_equal(L, ref) | (np.abs(L - ref) <= 1e-9 * np.maximum(np.abs(ref), 1e-12))
+    assert close.all(1).mean() >= 0.88
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["default", "big_light", "dielectric", "alt_open_space"])
+def test_render_vs_oracle_bitwise_e5(gpu_tracer, orc_vm, scene):
+    """renders sum a pixel's samples in the reference's order (chunk_spp is ignored for estimator 5)"""
+    sc = _e5_scene(scene)
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    o = orc_vm.render(40, 28, 20, 5, seed=SEED, chunk=20)
+    for chunk in (0, 7):
+        g = gpu_tracer.render(width=40, height=28, spp=20, estimator="surface_pt", seed=SEED, fp64=True,
+                              chunk_spp=chunk)
+        assert bitwise_equal(g, o).all()
+    assert np.abs(o).sum() > 0
+
+
+@pytest.mark.gpu
+def test_render_shards_e5(gpu_tracer):
+    """row bands compose to the whole image, bit for bit"""
+    gpu_tracer.set_scene(vpt.default_scene())
+    full = gpu_tracer.render(width=32, height=32, spp=3, estimator="surface_pt", seed=5, fp64=True)
+    parts = [gpu_tracer.render(width=32, height=32, spp=3, estimator="surface_pt", seed=5, fp64=True, band_rows=8,
+                               band_stride=2, band_offset=r) for r in range(2)]
+    rows = [[fr for b in range(r, 4, 2) for fr in range(b * 8, b * 8 + 8)] for r in range(2)]
+    for r in range(2):
+        assert bitwise_equal(parts[r], full[rows[r]]).all()
+
+
+@pytest.mark.gpu
+def test_count_work_matches_oracle_e5(gpu_tracer, orc_vm):
+    sc = EST_SCENES["big_light"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    t, it = gpu_tracer.count_work(vpt.RenderConfig(width=32, height=24, spp=4, estimator="surface_pt", seed=9))
+    _, c = orc_vm.render(32, 24, 4, 5, seed=9, counters=True, chunk=4)
+    assert (t, it) == (c.tests, c.iterations)
