@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define VPT_ABI_VERSION 1
+#define VPT_ABI_VERSION 2
 
 typedef enum {
     VPT_OK = 0,
@@ -67,12 +67,16 @@ typedef enum {
     VPT_EXPLICIT_FREE = 2,         /* explicitVPTracerRecursiveFree, vptShadeMethods.h:1153 */
     VPT_IMPLICIT_FREE = 3,         /* implicitVPTracerRecursiveFree, vptShadeMethods.h:940 */
     VPT_EXPLICIT_EQUIANGULAR = 4,  /* explicitVPTracerRecursive, vptShadeMethods.h:1014 */
-    VPT_SURFACE_PT = 5             /* iterativePathTracer, shadeMethods.h:104: surface-only path tracing (the
+    VPT_SURFACE_PT = 5,            /* iterativePathTracer, shadeMethods.h:104: surface-only path tracing (the
                                     * commented alternative at src/rt.cpp:793); sigma_a, sigma_s, hg_g and
                                     * max_depth are ignored; renders sum each pixel's samples in the
                                     * reference's sequential order (chunk_spp ignored) */
+    VPT_RAY_MARCHING = 6           /* rayMarching3, rayMarchingMethods.h:330: constant-step marching toward the
+                                    * light march_light (the commented alternative at src/rt.cpp:791, which
+                                    * passes sigma_a 0.001, sigma_s 0.0125, step 0.1, light 7); draws nothing
+                                    * beyond the camera jitter; samples summed in the reference's order */
 } vpt_estimator;
-#define VPT_NUM_ESTIMATORS 6
+#define VPT_NUM_ESTIMATORS 7
 
 typedef enum {
     VPT_FB_F32 = 0,            /* framebuffer: 3 x float per pixel */
@@ -86,6 +90,9 @@ typedef struct vpt_medium {
     double hg_g;               /* extension: Henyey-Greenstein g; 0 = the reference's isotropic phase */
     int32_t max_depth;         /* extension: max path vertices; 0 = unbounded (Russian roulette only) */
     int32_t estimator;         /* vpt_estimator */
+    double march_step;         /* VPT_RAY_MARCHING only: step length (> 0; default 0.1) */
+    int32_t march_light;       /* VPT_RAY_MARCHING only: index of the light sphere (default 7) */
+    int32_t reserved_;
 } vpt_medium;
 
 /* One image (or one shard of an image): main() of src/rt.cpp:744-830 made explicit. */

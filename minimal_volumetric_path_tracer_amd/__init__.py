@@ -2,7 +2,7 @@
 gabo99cas/minimal_volumetric_path_tracer (src/rt.cpp, include/vptShadeMethods.h) as HIP kernels
 for gfx950 behind a C ABI (include/vpt.h, libvpt.so).  See DESIGN.md."""
 from ._lib import (EXPLICIT_EQUIANGULAR, EXPLICIT_FREE, FB_F32, FB_F64, FREE_FLIGHT, IMPLICIT_FREE, MIS_EQUIANGULAR,
-                   RAY_DTYPE, SPHERE_DTYPE, SURFACE_PT, VPTError, lib)
+                   RAY_DTYPE, RAY_MARCHING, SPHERE_DTYPE, SURFACE_PT, VPTError, lib)
 from .tracer import (
     Ray,
     RenderConfig,
@@ -16,6 +16,6 @@ from .tracer import (
 )
 
 __all__ = [
-    "FB_F32", "FB_F64", "FREE_FLIGHT", "MIS_EQUIANGULAR", "EXPLICIT_FREE", "IMPLICIT_FREE", "EXPLICIT_EQUIANGULAR", "SURFACE_PT", "RAY_DTYPE", "SPHERE_DTYPE", "VPTError", "lib",
+    "FB_F32", "FB_F64", "FREE_FLIGHT", "MIS_EQUIANGULAR", "EXPLICIT_FREE", "IMPLICIT_FREE", "EXPLICIT_EQUIANGULAR", "SURFACE_PT", "RAY_MARCHING", "RAY_DTYPE", "SPHERE_DTYPE", "VPTError", "lib",
     "Ray", "RenderConfig", "Sphere", "Tracer", "default_scene", "encode_ppm", "scene", "stream_state", "write_ppm",
 ]

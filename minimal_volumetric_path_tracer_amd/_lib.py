@@ -20,7 +20,7 @@ CLI_PATH = os.path.join(PKG_DIR, "vpt")
 VPT_OK = 0
 VPT_E_INVALID, VPT_E_TOO_MANY, VPT_E_NO_EMITTER, VPT_E_UNSUPPORTED, VPT_E_HIP, VPT_E_IO = -1, -2, -3, -4, -5, -6
 VPT_MAX_SPHERES = 64
-FREE_FLIGHT, MIS_EQUIANGULAR, EXPLICIT_FREE, IMPLICIT_FREE, EXPLICIT_EQUIANGULAR, SURFACE_PT = 0, 1, 2, 3, 4, 5  # vpt_estimator
+FREE_FLIGHT, MIS_EQUIANGULAR, EXPLICIT_FREE, IMPLICIT_FREE, EXPLICIT_EQUIANGULAR, SURFACE_PT, RAY_MARCHING = 0, 1, 2, 3, 4, 5, 6  # vpt_estimator
 FB_F32, FB_F64 = 0, 1
 
 # numpy view of vpt_sphere == reference Sphere (include/Sphere.h:12-21), 144 bytes
@@ -46,6 +46,9 @@ class vpt_medium(ctypes.Structure):
         ("hg_g", c_double),
         ("max_depth", c_int32),
         ("estimator", c_int32),
+        ("march_step", c_double),
+        ("march_light", c_int32),
+        ("reserved_", c_int32),
     ]
 
 

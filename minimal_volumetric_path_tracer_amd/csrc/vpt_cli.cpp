@@ -1,7 +1,7 @@
 /*
  * vpt_cli.cpp -- the `vpt` program: drop-in for the reference's `./rt <spp>` (src/rt.cpp:744-830).
  *
- *   vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt] [--sigma-a A] [--sigma-s S]
+ *   vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt|ray-marching] [--march-step S] [--march-light I] [--sigma-a A] [--sigma-s S]
  *             [--g G] [--max-depth D] [--seed N] [--device I] [--fp64] [--out image.ppm]
  *
  * With only <spp> it renders the reference's default scene (include/Sphere.cpp:11-22), camera and
@@ -22,7 +22,7 @@
 static int usage()
 {
     std::fprintf(stderr,
-                 "usage: vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt] [--sigma-a A] [--sigma-s S]\n"
+                 "usage: vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt|ray-marching] [--march-step S] [--march-light I] [--sigma-a A] [--sigma-s S]\n"
                  "           [--g G] [--max-depth D] [--seed N] [--device I] [--fp64] [--out image.ppm]\n");
     return 2;
 }
@@ -58,8 +58,11 @@ int main(int argc, char** argv)
             else if (e == "implicit-free") p.medium.estimator = VPT_IMPLICIT_FREE;
             else if (e == "explicit") p.medium.estimator = VPT_EXPLICIT_EQUIANGULAR;
             else if (e == "surface-pt") p.medium.estimator = VPT_SURFACE_PT;
+            else if (e == "ray-marching") p.medium.estimator = VPT_RAY_MARCHING;
             else return usage();
-        } else if (a == "--sigma-a") p.medium.sigma_a = std::atof(need());
+        } else if (a == "--march-step") p.medium.march_step = std::atof(need());
+        else if (a == "--march-light") p.medium.march_light = std::atoi(need());
+        else if (a == "--sigma-a") p.medium.sigma_a = std::atof(need());
         else if (a == "--sigma-s") p.medium.sigma_s = std::atof(need());
         else if (a == "--g") p.medium.hg_g = std::atof(need());
         else if (a == "--max-depth") p.medium.max_depth = std::atoi(need());

@@ -985,6 +985,8 @@ VPT_DEV double equiangular_prob(double D, double ta, double tb, double s) { retu
 struct Medium {
     double sigma_a, sigma_s, g;
     int max_depth;
+    double march_step;  /* rayMarching3 only */
+    int march_light;
 };
 
 struct Path {
@@ -1212,12 +1214,57 @@ __device__ static dv3 trace_surface_pt(const DevScene* __restrict__ S, Sampler<C
     return Accum;
 }
 
+/* rayMarching3, include/rayMarchingMethods.h:330-384 (estimator 6): constant-step marching along the
+ * camera ray up to its first hit (no hit: black), single scattering from light m.march_light at
+ * every step i < t / step.  As written: step points measured from the ray origin (:351), their
+ * transmittance from the hit point x (:353); no random draw.  The shadow rays go through
+ * visibility() (a sphere light's own surface blocks them).  Steps per ray are capped at
+ * VPT_MARCH_MAX_STEPS (the reference has no cap) so that every wave ends; a capped ray returns NaN. */
+#ifndef VPT_MARCH_MAX_STEPS
+#define VPT_MARCH_MAX_STEPS (1 << 22)
+#endif
+template <bool COUNT>
+__device__ static dv3 trace_ray_marching(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d,
+                                         const Medium& m)
+{
+    const double sigma_a = m.sigma_a, sigma_s = m.sigma_s, step = m.march_step;
+    const int src = m.march_light;
+    double t;
+    int id = 0;
+    if (!scene_intersect(S, smp, o, d, t, id, false)) return mk(0, 0, 0);
+    const dv3 x = add(o, scl(d, t));
+    dv3 Li = mk(0, 0, 0);
+    const dv3 lp = sph_p(S, src);
+    const double lr = S->sph[src].r;
+    const bool l3 = S->geo[src].mat3;
+    const double steps = t / step;
+    if (!(steps < (double)VPT_MARCH_MAX_STEPS)) return mk(__builtin_nan(""), __builtin_nan(""), __builtin_nan(""));
+    for (int i = 0; i < steps; i++) {
+        if (COUNT) smp.cnt.iterations++;
+        const dv3 xt = add(o, scl(scl(d, step), (double)i));
+        const double T = transmitance(x, xt, sigma_a + sigma_s);
+        const double phase = 1 / (4 * VPT_PI);  /* isotropicPhaseFunction, volumetricBasicFunctions.h:59-62 */
+        const dv3 wc = sub(lp, xt);
+        const double normwc = dot(wc, wc);
+        if (visibility(S, smp, lp, xt, false, lr, l3)) {
+            const dv3 Le = scl(sph_rad(S, src), (1 / normwc));
+            const dv3 Ls = scl(Le, (phase * transmitance(xt, lp, sigma_a + sigma_s)));
+            Li = add(Li, scl(scl(scl(Ls, T), sigma_s), step));
+        } else {
+            Li = add(Li, mk(0, 0, 0));
+        }
+    }
+    return Li;
+}
+
 /* One camera sample, sequentially (the reference's per-sample call; used by vpt_trace_batch). */
 template <int EST, bool COUNT>
 __device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, const Medium& m)
 {
     if constexpr (EST == 5) {
         return trace_surface_pt<COUNT>(S, smp, o, d);
+    } else if constexpr (EST == 6) {
+        return trace_ray_marching<COUNT>(S, smp, o, d, m);
     } else {
         Path p;
         p.o = o;

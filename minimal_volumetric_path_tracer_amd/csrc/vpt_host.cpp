@@ -60,6 +60,8 @@ void vpt_default_params(vpt_params* p)
     p->medium.hg_g = 0.0;
     p->medium.max_depth = 0;
     p->medium.estimator = VPT_FREE_FLIGHT;
+    p->medium.march_step = 0.1;  /* rayMarching3's step and light at src/rt.cpp:791 */
+    p->medium.march_light = 7;
     p->seed = 0x5EED0001ull;
     /* Ray camera(Point(0, 11.2, 214), Vector(0, -0.042612, -1).normalize()) */
     double dx = 0, dy = -0.042612, dz = -1;

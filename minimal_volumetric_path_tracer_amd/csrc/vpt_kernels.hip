@@ -26,6 +26,8 @@ struct KParams {
     int32_t band_rows, band_stride, band_offset, shard_rows;
     double sigma_a, sigma_s, g;
     int32_t max_depth, est;
+    double march_step;             /* rayMarching3 (estimator 6) */
+    int32_t march_light;
     uint64_t seed;
     double o[3], d[3], cx[3], cy[3];
     void* out;
@@ -55,7 +57,7 @@ __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const Dev
     const int fr = (P.band_offset + k * P.band_stride) * P.band_rows + r;  /* file row */
     const int y = P.h - 1 - fr;                                              /* camera row */
     const uint64_t idx = (uint64_t)fr * (uint64_t)P.w + (uint64_t)x;          /* src/rt.cpp:773 */
-    const Medium m{P.sigma_a, P.sigma_s, P.g, P.max_depth};
+    const Medium m{P.sigma_a, P.sigma_s, P.g, P.max_depth, P.march_step, P.march_light};
     const dv3 o = mk(P.o[0], P.o[1], P.o[2]), cd = mk(P.d[0], P.d[1], P.d[2]);
     const dv3 cx = mk(P.cx[0], P.cx[1], P.cx[2]), cy = mk(P.cy[0], P.cy[1], P.cy[2]);
     dv3 acc = mk(0, 0, 0);
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P, const DevScene* 
 {
     const int lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
-    const Medium m{P.sigma_a, P.sigma_s, P.g, P.max_depth};
+    const Medium m{P.sigma_a, P.sigma_s, P.g, P.max_depth, P.march_step, P.march_light};
     const dv3 o0 = mk(P.o[0], P.o[1], P.o[2]);
     const unsigned npix = (unsigned)P.tiles_x * (unsigned)P.tiles_y * 64u;
 
@@ -324,6 +326,17 @@ static int check_medium(const vpt_medium* m)
     return VPT_OK;
 }
 
+/* rayMarching3's step and light (estimator 6 only): the light must be a sphere of the scene */
+static int check_march(const vpt_context* ctx, const vpt_medium* m)
+{
+    if (m->estimator != VPT_RAY_MARCHING) return VPT_OK;
+    if (!is_finite(m->march_step) || !(m->march_step > 0))
+        return vpt_fail(VPT_E_INVALID, "march_step must be finite and > 0");
+    if (m->march_light < 0 || m->march_light >= ctx->h_scene.n)
+        return vpt_fail(VPT_E_INVALID, "march_light %d is not a sphere of the scene (%d)", m->march_light, ctx->h_scene.n);
+    return VPT_OK;
+}
+
 static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_out, KParams& K)
 {
     if (!ctx || !p) return vpt_fail(VPT_E_INVALID, "NULL context or params");
@@ -332,6 +345,7 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
     if ((int64_t)p->width * p->height > (int64_t)1 << 31) return vpt_fail(VPT_E_INVALID, "image too large");
     if (p->fb_format != VPT_FB_F32 && p->fb_format != VPT_FB_F64) return vpt_fail(VPT_E_INVALID, "bad fb_format");
     int rc = check_medium(&p->medium);
+    if (!rc) rc = check_march(ctx, &p->medium);
     if (rc) return rc;
     if (p->band_rows <= 0 || p->band_stride <= 0 || p->band_offset < 0 || p->band_offset >= p->band_stride)
         return vpt_fail(VPT_E_INVALID, "bad band_rows/band_stride/band_offset");
@@ -353,6 +367,8 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
     K.g = p->medium.hg_g;
     K.max_depth = p->medium.max_depth;
     K.est = p->medium.estimator;
+    K.march_step = p->medium.march_step;
+    K.march_light = p->medium.march_light;
     K.seed = p->seed;
     for (int i = 0; i < 3; ++i) {
         K.o[i] = p->camera.o[i];
@@ -414,8 +430,8 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         HIP_OK(hipGetLastError());
         return VPT_OK;
     }
-    if constexpr (!COUNT && EST != 5) return launch_pool<EST, FB>(ctx, K, stream);
-    if constexpr (EST == 5) {  /* iterativePathTracer: one lane per pixel, samples summed in order */
+    if constexpr (!COUNT && EST < 5) return launch_pool<EST, FB>(ctx, K, stream);
+    if constexpr (EST >= 5) {  /* iterativePathTracer, rayMarching3: one lane per pixel, samples summed in order */
         dim3 grid((unsigned)((K.w + 15) / 16), (unsigned)((K.shard_rows + 15) / 16));
         render_kernel_simple<EST, COUNT, FB><<<grid, dim3(256), 0, stream>>>(K, S);
         HIP_OK(hipGetLastError());
@@ -465,7 +481,7 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         }
         Q.partials = ctx->d_partials;
         Q.queue = ctx->d_queue;
-        const Medium m{K.sigma_a, K.sigma_s, K.g, K.max_depth};
+        const Medium m{K.sigma_a, K.sigma_s, K.g, K.max_depth, K.march_step, K.march_light};
         rc = persistent_grid(ctx, pool_kernel<EST, COUNT>, &blocks);
         if (rc) return rc;
         const uint64_t need = (units + POOL - 1) / POOL;
@@ -526,6 +542,7 @@ static int launch_render(vpt_context* ctx, KParams K, hipStream_t stream)
         VPT_LAUNCH_EST(3)
         VPT_LAUNCH_EST(4)
         VPT_LAUNCH_EST(5)
+        VPT_LAUNCH_EST(6)
     }
 #undef VPT_LAUNCH_EST
     return vpt_fail(VPT_E_INVALID, "unknown estimator %d", K.est);
@@ -684,6 +701,7 @@ int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, 
     if (!ctx || !rays || !states || !out_rgb || n < 0) return vpt_fail(VPT_E_INVALID, "vpt_trace_batch: bad arguments");
     if (!ctx->has_scene) return vpt_fail(VPT_E_INVALID, "no scene set (vpt_set_scene)");
     int rc = check_medium(m);
+    if (!rc) rc = check_march(ctx, m);
     if (rc) return rc;
     if (n == 0) return VPT_OK;
     HIP_OK(hipSetDevice(ctx->device));
@@ -697,7 +715,7 @@ int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, 
     if (e == hipSuccess) e = hipMemcpy(dr, rays, sizeof(vpt_ray) * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(ds, states, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        Medium mm{m->sigma_a, m->sigma_s, m->hg_g, m->max_depth};
+        Medium mm{m->sigma_a, m->sigma_s, m->hg_g, m->max_depth, m->march_step, m->march_light};
         dim3 grid((unsigned)((n + 255) / 256)), block(256);
         switch (m->estimator) {
         case 0: trace_batch_kernel<0><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
@@ -705,7 +723,8 @@ int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, 
         case 2: trace_batch_kernel<2><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         case 3: trace_batch_kernel<3><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         case 4: trace_batch_kernel<4><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
-        default: trace_batch_kernel<5><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        case 5: trace_batch_kernel<5><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        default: trace_batch_kernel<6><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         }
         e = hipGetLastError();
     }

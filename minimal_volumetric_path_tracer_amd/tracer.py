@@ -24,11 +24,12 @@ import numpy as np
 
 from . import _lib
 from ._lib import (EXPLICIT_EQUIANGULAR, EXPLICIT_FREE, FB_F32, FB_F64, FREE_FLIGHT, IMPLICIT_FREE, MIS_EQUIANGULAR,
-                   RAY_DTYPE, SPHERE_DTYPE, SURFACE_PT, check, lib)
+                   RAY_DTYPE, RAY_MARCHING, SPHERE_DTYPE, SURFACE_PT, check, lib)
 
 ESTIMATORS = {"ff": FREE_FLIGHT, "free_flight": FREE_FLIGHT, "mis": MIS_EQUIANGULAR, "mis_equiangular": MIS_EQUIANGULAR,
               "explicit_free": EXPLICIT_FREE, "implicit_free": IMPLICIT_FREE, "explicit": EXPLICIT_EQUIANGULAR,
-              "explicit_equiangular": EXPLICIT_EQUIANGULAR, "surface_pt": SURFACE_PT, "path_tracer": SURFACE_PT}
+              "explicit_equiangular": EXPLICIT_EQUIANGULAR, "surface_pt": SURFACE_PT, "path_tracer": SURFACE_PT,
+              "ray_marching": RAY_MARCHING}
 
 
 def Sphere(r, p, c=(0, 0, 0), radiance=(0, 0, 0), material=0, eta=(0, 0, 0), kappa=(0, 0, 0), alpha=0.0) -> np.ndarray:
@@ -78,6 +79,8 @@ class RenderConfig:
     band_stride: int = 1
     band_offset: int = 0
     chunk_spp: int = 0          # 0 = auto (min(spp, 32), the last 64 samples tapered); 1 or >= spp = the reference's sequential sum
+    march_step: float = 0.1     # rayMarching3 (estimator "ray_marching") only: step (src/rt.cpp:791)
+    march_light: int = 7        # rayMarching3 only: light sphere index (src/rt.cpp:791)
 
     def params(self) -> _lib.vpt_params:
         p = _lib.vpt_params()
@@ -87,6 +90,7 @@ class RenderConfig:
         p.medium.sigma_a, p.medium.sigma_s = self.sigma_a, self.sigma_s
         p.medium.hg_g, p.medium.max_depth = self.hg_g, self.max_depth
         p.medium.estimator = ESTIMATORS[self.estimator] if isinstance(self.estimator, str) else int(self.estimator)
+        p.medium.march_step, p.medium.march_light = self.march_step, self.march_light
         p.seed = self.seed
         p.band_rows = self.band_rows if self.band_rows > 0 else self.height
         p.band_stride, p.band_offset = self.band_stride, self.band_offset
@@ -150,9 +154,10 @@ class Tracer:
 
     # ---- the per-sample estimators, batched ----
     def trace(self, estimator, rays: np.ndarray, states: np.ndarray, sigma_a=0.001, sigma_s=0.009, hg_g=0.0,
-              max_depth=0) -> tuple[np.ndarray, np.ndarray]:
+              max_depth=0, march_step=0.1, march_light=7) -> tuple[np.ndarray, np.ndarray]:
         m = _lib.vpt_medium(sigma_a, sigma_s, hg_g, max_depth,
-                            ESTIMATORS[estimator] if isinstance(estimator, str) else int(estimator))
+                            ESTIMATORS[estimator] if isinstance(estimator, str) else int(estimator), march_step,
+                            march_light)
         r = np.ascontiguousarray(rays, dtype=RAY_DTYPE)
         s = np.ascontiguousarray(states, dtype=np.uint64)
         if len(r) != len(s):
@@ -186,6 +191,10 @@ class Tracer:
     def iterativePathTracer(self, rays, states):
         """Batched include/shadeMethods.h:104 (surface only: no medium arguments)."""
         return self.trace("surface_pt", rays, states)
+
+    def rayMarching3(self, rays, states, sigma_a, sigma_s, step, idsource):
+        """Batched include/rayMarchingMethods.h:330 (src/rt.cpp:791 passes 0.001, 0.0125, 0.1, 7)."""
+        return self.trace("ray_marching", rays, states, sigma_a, sigma_s, march_step=step, march_light=idsource)
 
     def math_probe(self, fn: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float64)

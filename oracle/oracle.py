@@ -21,7 +21,7 @@ SPHERE_BYTES = 144
 
 class Medium(ctypes.Structure):
     _fields_ = [("sigma_a", c_double), ("sigma_s", c_double), ("hg_g", c_double), ("max_depth", c_int32),
-                ("estimator", c_int32)]
+                ("estimator", c_int32), ("march_step", c_double), ("march_light", c_int32), ("reserved_", c_int32)]
 
 
 class Counters(ctypes.Structure):
@@ -104,8 +104,8 @@ class Oracle:
             raise ValueError("oracle: bad scene")
 
     def trace(self, estimator: int, rays: np.ndarray, states: np.ndarray, sigma_a=0.001, sigma_s=0.009, hg_g=0.0,
-              max_depth=0, counters: bool = False):
-        m = Medium(sigma_a, sigma_s, hg_g, max_depth, estimator)
+              max_depth=0, counters: bool = False, march_step=0.1, march_light=7):
+        m = Medium(sigma_a, sigma_s, hg_g, max_depth, estimator, march_step, march_light)
         r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
         out = np.zeros((len(r), 3))
         st = np.zeros(len(r), dtype=np.uint64)
@@ -119,12 +119,12 @@ class Oracle:
         return (out, st, tot) if counters else (out, st)
 
     def render(self, w, h, spp, estimator=0, sigma_a=0.001, sigma_s=0.009, hg_g=0.0, max_depth=0, seed=0x5EED0001,
-               y0=0, y1=None, threads=0, counters=False, chunk=None):
+               y0=0, y1=None, threads=0, counters=False, chunk=None, march_step=0.1, march_light=7):
         """main()'s pixel loop over camera rows [y0, y1); returns (h, w, 3) float64 in file order.
         chunk: samples per partial sum in uniform chunks (spp = the reference's order); None = the
         GPU's default (vpt_params.chunk_spp == 0): chunks of min(spp, 32), the last 32 tapered
         (csrc/vpt_chunks.h)."""
-        m = Medium(sigma_a, sigma_s, hg_g, max_depth, estimator)
+        m = Medium(sigma_a, sigma_s, hg_g, max_depth, estimator, march_step, march_light)
         out = np.zeros((h, w, 3))
         c = Counters()
         taper = 0
@@ -174,6 +174,7 @@ class Reference:
         L.ref_render.restype = None
         L.ref_render.argtypes = [_I, _I, _I, _I, _D, _D, _U, _I, _I, _P, _P]
         L.ref_sizeof_sphere.restype = _I
+        L.ref_set_march.restype, L.ref_set_march.argtypes = None, [_D, _I]
         self.L = L
         self.prefix = "ref"
 
@@ -191,7 +192,8 @@ class Reference:
         b = np.ascontiguousarray(spheres).view(np.uint8)
         self.L.ref_set_scene(b.ctypes.data, len(b) // SPHERE_BYTES)
 
-    def trace(self, estimator, rays, states, sigma_a=0.001, sigma_s=0.009):
+    def trace(self, estimator, rays, states, sigma_a=0.001, sigma_s=0.009, march_step=0.1, march_light=7):
+        self.L.ref_set_march(march_step, march_light)
         r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
         out = np.zeros((len(r), 3))
         st = np.zeros(len(r), dtype=np.uint64)
@@ -200,7 +202,8 @@ class Reference:
         return out, st
 
     def render(self, w, h, spp, estimator=0, sigma_a=0.001, sigma_s=0.009, seed=0x5EED0001, y0=0, y1=None,
-               per_sample=False):
+               per_sample=False, march_step=0.1, march_light=7):
+        self.L.ref_set_march(march_step, march_light)
         out = np.zeros((h, w, 3))
         ps = np.zeros((h * w * spp, 3)) if per_sample else None
         self.L.ref_render(w, h, spp, estimator, sigma_a, sigma_s, seed, y0, h if y1 is None else y1, out.ctypes.data,

@@ -31,6 +31,7 @@
 #include "vptSamplingFunctions.h"
 #include "vptShadeMethods.h"
 #include "shadeMethods.h"
+#include "rayMarchingMethods.h"
 
 extern "C" {
 #include "oracle_rng.h"
@@ -105,7 +106,10 @@ void ref_set_scene(const void* in, int n)
  *   2 explicitVPTracerRecursiveFree  vptShadeMethods.h:1153
  *   3 implicitVPTracerRecursiveFree  vptShadeMethods.h:938
  *   4 explicitVPTracerRecursive      vptShadeMethods.h:1014
- *   5 iterativePathTracer            shadeMethods.h:104 (surface only: sa, ss unused) */
+ *   5 iterativePathTracer            shadeMethods.h:104 (surface only: sa, ss unused)
+ *   6 rayMarching3                   rayMarchingMethods.h:330 (step, idsource: ref_set_march) */
+static double g_march_step = 0.1;  /* src/rt.cpp:791 */
+static int g_march_light = 7;
 static Color run_estimator(int estimator, const Ray& r, double sa, double ss)
 {
     switch (estimator) {
@@ -114,12 +118,19 @@ static Color run_estimator(int estimator, const Ray& r, double sa, double ss)
     case 2: return explicitVPTracerRecursiveFree(r, sa, ss, 0);
     case 3: return implicitVPTracerRecursiveFree(r, sa, ss);
     case 4: return explicitVPTracerRecursive(r, sa, ss, 0);
-    default: return iterativePathTracer(r);
+    case 5: return iterativePathTracer(r);
+    default: return rayMarching3(r, sa, ss, g_march_step, g_march_light);
     }
 }
 
 /* One camera sample through an estimator.  `state` is the erand48 state before the call; the
  * state after the call is returned (tells how many draws were consumed). */
+void ref_set_march(double step, int light)
+{
+    g_march_step = step;
+    g_march_light = light;
+}
+
 uint64_t ref_trace(int estimator, const double ray[6], uint64_t state, double sa, double ss,
                    double out[3])
 {

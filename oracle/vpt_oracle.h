@@ -28,7 +28,10 @@ typedef struct {
     double sigma_a, sigma_s;  /* src/rt.cpp:794 */
     double hg_g;              /* extension: 0 = reference isotropic phase */
     int32_t max_depth;        /* extension: 0 = unbounded (reference) */
-    int32_t estimator;        /* include/vpt.h vpt_estimator: 0 iterativeVPTracerFree, 1 MISVPTTracerRecursive, ..., 5 iterativePathTracer */
+    int32_t estimator;        /* include/vpt.h vpt_estimator: 0 iterativeVPTracerFree, 1 MISVPTTracerRecursive, ..., 5 iterativePathTracer, 6 rayMarching3 */
+    double march_step;        /* rayMarching3: step */
+    int32_t march_light;      /* rayMarching3: idsource */
+    int32_t reserved_;
 } orc_medium;
 
 typedef struct {           /* work counters (counting mode) */

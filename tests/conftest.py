@@ -56,6 +56,12 @@ def samples_e5():
 
 
 @pytest.fixture(scope="session")
+def samples_e6():
+    """rayMarching3 (estimator 6) cases of make_golden.py MARCH_CASES (make_golden.py --ray-marching)"""
+    return dict(np.load(os.path.join(GOLDEN, "samples_e6.npz")))
+
+
+@pytest.fixture(scope="session")
 def prims():
     return dict(np.load(os.path.join(GOLDEN, "primitives.npz")))
 

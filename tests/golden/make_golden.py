@@ -275,6 +275,40 @@ def surface_pt():
     print("wrote", os.path.join(HERE, "samples_e5.npz"))
 
 
+# rayMarching3 cases: (scene, light index, step); sigma_a 0.001, sigma_s 0.0125 as src/rt.cpp:791
+MARCH_CASES = [("default", 8, 0.1), ("default", 7, 0.1), ("alt_metal_walls", 7, 0.25), ("alt_open_space", 4, 0.5),
+               ("alt_light_near_camera", 2, 0.5)]
+
+
+def ray_marching():
+    """rayMarching3 (include/rayMarchingMethods.h:330, estimator 6) -> samples_e6.npz."""
+    ref = Reference()
+    rng = np.random.default_rng(20261018)
+    scenes = {**EST_SCENES, **ALT_SCENES}
+    bundle = {}
+    for name, light, step in MARCH_CASES:
+        sc = scenes[name]()
+        ref.set_scene(sc)
+        key = f"{name}_l{light}"
+        bundle[f"{key}__scene"] = sc.view(np.uint8)
+        bundle[f"{key}__march"] = np.array([step, light])
+        ref.L.ref_set_march(step, light)
+        xs, ys, si = rng.integers(0, W, 96), rng.integers(0, H, 96), rng.integers(0, 1 << 20, 96)
+        s0 = np.array([stream_state(SEED, int((H - y - 1) * W + x), int(i)) for x, y, i in zip(xs, ys, si)],
+                      dtype=np.uint64)
+        rays = np.zeros((96, 6))
+        s1 = np.zeros(96, dtype=np.uint64)
+        for k in range(96):
+            s1[k] = ref.prim("camera_ray")(W, H, int(xs[k]), int(ys[k]), int(s0[k]), rays[k].ctypes.data)
+        out, s2 = ref.trace(6, rays, s1, 0.001, 0.0125, march_step=step, march_light=light)
+        bundle.update({f"{key}__e6__ray": rays, f"{key}__e6__state1": s1, f"{key}__e6__L": out,
+                       f"{key}__e6__state2": s2})
+        bundle[f"{key}__e6__fb24x24x2"] = ref.render(24, 24, 2, 6, 0.001, 0.0125, seed=SEED, march_step=step,
+                                                     march_light=light)
+    np.savez_compressed(os.path.join(HERE, "samples_e6.npz"), **bundle)
+    print("wrote", os.path.join(HERE, "samples_e6.npz"))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["--estimators-234"]:
         estimators_234()
@@ -282,8 +316,11 @@ if __name__ == "__main__":
         alt_scenes()
     elif sys.argv[1:] == ["--surface-pt"]:
         surface_pt()
+    elif sys.argv[1:] == ["--ray-marching"]:
+        ray_marching()
     else:
         main()
         estimators_234()
         alt_scenes()
         surface_pt()
+        ray_marching()

@@ -29,7 +29,7 @@ def test_exports_every_declared_symbol():
         assert hasattr(L, n), n
     bound = {p[0] for p in _lib.PROTOTYPES}
     assert bound == set(names), set(names) ^ bound
-    assert vpt.lib().vpt_abi_version() == 1
+    assert vpt.lib().vpt_abi_version() == 2
 
 
 def test_struct_layouts():
@@ -38,8 +38,8 @@ def test_struct_layouts():
     assert offs == {"r": 0, "p": 8, "c": 32, "radiance": 56, "material": 80, "reserved_": 84, "eta": 88,
                     "kappa": 112, "alpha": 136}
     assert ctypes.sizeof(_lib.vpt_ray) == 48
-    assert ctypes.sizeof(_lib.vpt_medium) == 32
-    assert ctypes.sizeof(_lib.vpt_params) == 16 + 32 + 8 + 48 + 8 + 16
+    assert ctypes.sizeof(_lib.vpt_medium) == 48
+    assert ctypes.sizeof(_lib.vpt_params) == 16 + 48 + 8 + 48 + 8 + 16
 
 
 def test_default_scene_is_reference_scene():

@@ -450,3 +450,63 @@ def test_count_work_matches_oracle_e5(gpu_tracer, orc_vm):
     t, it = gpu_tracer.count_work(vpt.RenderConfig(width=32, height=24, spp=4, estimator="surface_pt", seed=9))
     _, c = orc_vm.render(32, 24, 4, 5, seed=9, counters=True, chunk=4)
     assert (t, it) == (c.tests, c.iterations)
+
+
+# ---------------------------------------------------------------- estimator 6: rayMarching3
+E6_CASES = ["default_l8", "default_l7", "alt_metal_walls_l7", "alt_open_space_l4", "alt_light_near_camera_l2"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", E6_CASES)
+def test_trace_batch_vs_oracle_bitwise_e6(gpu_tracer, orc_vm, samples_e6, case):
+    """include/rayMarchingMethods.h:330 per sample: same bits as the oracle, no draw consumed"""
+    sc = samples_e6[f"{case}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    step, light = samples_e6[f"{case}__march"]
+    k = f"{case}__e6__"
+    rays, st = samples_e6[k + "ray"], samples_e6[k + "state1"]
+    L, s = gpu_tracer.rayMarching3(_rays(rays), st, 0.001, 0.0125, step, int(light))
+    Lo, so = orc_vm.trace(6, rays, st, 0.001, 0.0125, march_step=step, march_light=int(light))
+    assert np.array_equal(s, so) and np.array_equal(s, st)
+    same = bitwise_equal(L, Lo)
+    assert same.all(), f"{(~same.all(1)).sum()} of {len(L)} samples differ"
+    # against the reference's own values: the portable libm (exp, sqrt-based normalise) may differ
+    # from glibc by an ulp, which moves no branch here but can move a last bit
+    ref = samples_e6[k + "L"]
+    assert (np.abs(L - ref) <= 1e-12 * np.maximum(np.abs(ref), 1e-300)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["default_l8", "alt_light_near_camera_l2"])
+def test_render_vs_oracle_bitwise_e6(gpu_tracer, orc_vm, samples_e6, case):
+    sc = samples_e6[f"{case}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    step, light = samples_e6[f"{case}__march"]
+    g = gpu_tracer.render(width=24, height=24, spp=2, estimator="ray_marching", sigma_a=0.001, sigma_s=0.0125,
+                          march_step=float(step), march_light=int(light), seed=SEED, fp64=True)
+    o = orc_vm.render(24, 24, 2, 6, 0.001, 0.0125, seed=SEED, chunk=2, march_step=step, march_light=int(light))
+    assert bitwise_equal(g, o).all()
+    ref = samples_e6[f"{case}__e6__fb24x24x2"]
+    assert (np.abs(g - ref) <= 1e-12 * np.maximum(np.abs(ref), 1e-300)).all()
+
+
+@pytest.mark.gpu
+def test_count_work_matches_oracle_e6(gpu_tracer, orc_vm):
+    sc = vpt.default_scene()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    cfg = vpt.RenderConfig(width=16, height=12, spp=2, estimator="ray_marching", march_step=0.5, march_light=8, seed=9)
+    t, it = gpu_tracer.count_work(cfg)
+    _, c = orc_vm.render(16, 12, 2, 6, seed=9, counters=True, chunk=2, march_step=0.5, march_light=8)
+    assert (t, it) == (c.tests, c.iterations)
+
+
+@pytest.mark.gpu
+def test_ray_marching_invalid_arguments(gpu_tracer):
+    gpu_tracer.set_scene(vpt.default_scene())
+    for kw in (dict(march_step=0.0), dict(march_step=-1.0), dict(march_step=float("nan")), dict(march_light=10),
+               dict(march_light=-1)):
+        with pytest.raises(vpt.VPTError):
+            gpu_tracer.render(width=8, height=8, spp=1, estimator="ray_marching", **kw)

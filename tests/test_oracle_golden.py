@@ -274,3 +274,24 @@ def test_surface_pt_vs_reference(samples_e5, orc, scene):
     # no emitter, or (alt_area_light) a light with radiance.x == 0, which iterativePathTracer and MIS
     # never treat as a light (include/shadeMethods.h:122, include/misSamplingFunctions.h:29)
     assert (samples_e5[k + "L"] != 0).any() == (scene not in ("no_emitter", "alt_area_light"))
+
+
+# ---- rayMarching3 (include/rayMarchingMethods.h:330): estimator 6, no random draw past the camera jitter
+E6_CASES = ["default_l8", "default_l7", "alt_metal_walls_l7", "alt_open_space_l4", "alt_light_near_camera_l2"]
+
+
+@pytest.mark.parametrize("case", E6_CASES)
+def test_ray_marching_vs_reference(samples_e6, orc, case):
+    orc.set_scene(samples_e6[f"{case}__scene"])
+    step, light = samples_e6[f"{case}__march"]
+    k = f"{case}__e6__"
+    L, st = orc.trace(6, samples_e6[k + "ray"], samples_e6[k + "state1"], 0.001, 0.0125, march_step=step,
+                      march_light=int(light))
+    assert np.array_equal(st, samples_e6[k + "state1"]) and np.array_equal(st, samples_e6[k + "state2"])
+    assert bitwise_equal(L, samples_e6[k + "L"]).all()
+    out = orc.render(24, 24, 2, 6, 0.001, 0.0125, seed=SEED, threads=2, chunk=2, march_step=step,
+                     march_light=int(light))
+    assert bitwise_equal(out, samples_e6[k + "fb24x24x2"]).all()
+    # light 7 of the default scene is a sphere light (r = 2): its shadow rays start at its centre and
+    # stop on its own surface, so the reference's marching sees it nowhere
+    assert (np.abs(out).sum() > 0) == (case != "default_l7")
