@@ -131,7 +131,9 @@ struct PoolParams {
     unsigned nunits;
     uint64_t seed;
     double o[3], d[3], cx[3], cy[3];
-    double* partials;       /* rows * w * nch * 3 */
+    double* partials;       /* nch * rows * w * 3: chunk-major, so the units of one chunk level (handed
+                             * out together, 8x8 tiles) write neighbouring 24-B records that merge into
+                             * whole lines in L2 (pixel-major wrote 24 B per 128-B line: 2x the WRITE_SIZE) */
     unsigned* queue;
 };
 
@@ -232,7 +234,7 @@ __device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, b
     }
 }
 
-/* the finished unit's chunk sum -> partials[shard row][x][chunk] */
+/* the finished unit's chunk sum -> partials[chunk][shard row][x] */
 __device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t)
 {
     const int x = (int)(t.pix & 0xFFFFu), y = (int)(t.pix >> 16);
@@ -240,7 +242,7 @@ __device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t
     const int k = fr / P.band_rows, rr = fr - k * P.band_rows;
     const int lr = ((k - P.band_offset) / P.band_stride) * P.band_rows + rr;
     const int c = vpt_chunk_of_end(&P.lay, (int)t.c1);
-    const size_t o = (((size_t)lr * (size_t)P.w + (size_t)x) * (size_t)P.nch + (size_t)c) * 3;
+    const size_t o = (((size_t)c * (size_t)P.rows + (size_t)lr) * (size_t)P.w + (size_t)x) * 3;
     P.partials[o] = t.acc.x;
     P.partials[o + 1] = t.acc.y;
     P.partials[o + 2] = t.acc.z;
@@ -735,9 +737,10 @@ __global__ __launch_bounds__(256) void reduce_kernel(PoolParams P, void* out)
     const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
     const size_t npix = (size_t)P.rows * (size_t)P.w;
     if (p >= npix) return;
-    const double* q = P.partials + p * (size_t)P.nch * 3;
+    const double* q = P.partials + p * 3;
+    const size_t plane = npix * 3;  /* one chunk level (chunk-major layout, store_partial) */
     dv3 tot = mk(0, 0, 0);
-    for (int c = 0; c < P.nch; ++c) tot = add(mk(q[3 * c], q[3 * c + 1], q[3 * c + 2]), tot);
+    for (int c = 0; c < P.nch; ++c) tot = add(mk(q[c * plane], q[c * plane + 1], q[c * plane + 2]), tot);
     tot = scl(tot, (1 / (double)P.spp));  /* src/rt.cpp:800 */
     if (FB == VPT_FB_F32) {
         float* o = (float*)out;

@@ -4,7 +4,7 @@
 set -u
 TAG=${1:-r01}
 shift || true
-ARGS=${*:---steps 1 --warmup 0 --no-cpu}
+ARGS=${*:---steps 1 --warmup 0 --no-cpu --inflight 1}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
