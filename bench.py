@@ -46,6 +46,8 @@ CONFIGS = {
     "mis": dict(width=1024, height=1024, spp=1024, estimator="mis", sigma_a=0.001, sigma_s=0.009, hg_g=0.5),
     # BASELINE.json configs[3]: dense medium, 8 bounces
     "dense": dict(width=2048, height=2048, spp=4096, estimator="ff", sigma_a=0.01, sigma_s=0.09, max_depth=8),
+    # BASELINE.json configs[4]: meant for --gpus 8 (137 G samples per image; ~4 s per step on 8 GPUs)
+    "mis4k": dict(width=4096, height=4096, spp=8192, estimator="mis", sigma_a=0.001, sigma_s=0.009),
 }
 
 
@@ -154,7 +156,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="ff", choices=list(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--chunk", type=int, default=0, help="samples per work unit (0 = auto, min(spp, 32))")
+    ap.add_argument("--chunk", type=int, default=0, help="samples per work unit (0 = auto: 32, more above 4096 spp, tapered; vpt_chunks.h)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="steps in flight: each on its own context + HIP stream, so one launch's drain (its "
                          "last, longest paths) overlaps the next launch's start; 1 = strictly serialized")

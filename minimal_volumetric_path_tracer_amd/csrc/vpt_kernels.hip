@@ -391,7 +391,7 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
     /* auto: 32 samples per work unit (A/B at 1024^2 x 256: chunk 4 / 8 / 16 / 32 / 64 -> 3816 / 3969 /
      * 4085 / 4153 / 4129 Ms/s), the last 32 of a pixel tapered (vpt_chunks.h); spp <= 32 is then one
      * chunk, i.e. the reference's sequential sum.  An explicit chunk_spp gives uniform chunks. */
-    K.chunk = p->chunk_spp > 0 ? (p->chunk_spp < p->spp ? p->chunk_spp : p->spp) : (p->spp < 32 ? p->spp : 32);
+    K.chunk = p->chunk_spp > 0 ? (p->chunk_spp < p->spp ? p->chunk_spp : p->spp) : vpt_auto_chunk(p->spp);
     K.taper = p->chunk_spp == 0;
     return VPT_OK;
 }

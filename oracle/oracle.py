@@ -67,8 +67,8 @@ def _bind(L: ctypes.CDLL, prefix: str) -> ctypes.CDLL:
 
 
 def default_chunk(spp: int) -> int:
-    """samples per chunk the GPU uses when vpt_params.chunk_spp == 0 (csrc/vpt_kernels.hip)"""
-    return min(spp, 32)
+    """samples per chunk the GPU uses when vpt_params.chunk_spp == 0 (vpt_auto_chunk, csrc/vpt_chunks.h)"""
+    return min(spp, max(32, -(-spp // 128)))
 
 
 class Oracle:

@@ -59,3 +59,18 @@ def test_tapered_render_is_a_reordered_sum(orc):
     c = orc.render(8, 6, 40, 0, seed=9, threads=2, chunk=32)    # uniform chunks
     assert np.allclose(a, b, rtol=1e-12, atol=1e-14) and np.allclose(a, c, rtol=1e-12, atol=1e-14)
     assert not np.array_equal(a, c) or not np.array_equal(a, b)  # the layouts do differ somewhere
+
+
+def test_auto_chunk_size(orc):
+    """the GPU's auto chunk size (vpt_auto_chunk, shared header) and the oracle's Python mirror agree;
+    32 up to 4096 spp, then at most 128 chunks + the taper (work units of a 4096^2 x 8192 image < 2^32)"""
+    from oracle.oracle import default_chunk
+
+    orc.L.orc_auto_chunk.restype = ctypes.c_int
+    orc.L.orc_auto_chunk.argtypes = [ctypes.c_int]
+    for spp in list(range(1, 300)) + [1023, 1024, 4095, 4096, 4097, 8192, 65536, 1 << 20]:
+        c = orc.L.orc_auto_chunk(spp)
+        assert c == default_chunk(spp), spp
+        assert c == min(spp, 32) or (spp > 4096 and c == -(-spp // 128))
+    n = len(layout(orc, 8192, orc.L.orc_auto_chunk(8192), 1)) - 1
+    assert 4096 * 4096 * n < 2**32 and n <= 128 + 16

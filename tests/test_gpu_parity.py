@@ -510,3 +510,15 @@ def test_ray_marching_invalid_arguments(gpu_tracer):
                dict(march_light=-1)):
         with pytest.raises(vpt.VPTError):
             gpu_tracer.render(width=8, height=8, spp=1, estimator="ray_marching", **kw)
+
+
+@pytest.mark.gpu
+def test_large_spp_auto_chunk(gpu_tracer, orc_vm):
+    """above 4096 spp the auto chunk grows (vpt_auto_chunk: 5000 spp -> 40-sample chunks + taper);
+    same sums as the oracle's layout"""
+    sc = SCENES["default"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    g = gpu_tracer.render(width=8, height=6, spp=5000, seed=12, fp64=True)
+    o = orc_vm.render(8, 6, 5000, 0, seed=12, threads=4)
+    assert bitwise_equal(g, o).all()
