@@ -11,13 +11,14 @@ cname = sys.argv[1] if len(sys.argv) > 1 else "ff"
 Ns = [int(a) for a in sys.argv[2:]] or [1, 8]
 c = CONFIGS[cname]
 K = int(os.environ.get("STEPS", "12"))
-trs = [vpt.Tracer(0) for _ in range(3)]
-streams = [torch.cuda.Stream() for _ in range(3)]
+DEPTHS = [int(x) for x in os.environ.get("DEPTHS", "1,2,3").split(",")]
+trs = [vpt.Tracer(0) for _ in range(max(DEPTHS))]
+streams = [torch.cuda.Stream() for _ in range(max(DEPTHS))]
 for N in Ns:
     cfg = vpt.RenderConfig(**c, seed=0x5EED0001, band_rows=16 if N > 1 else c["height"], band_stride=N, band_offset=0)
-    outs = [torch.empty((cfg.shard_rows(), c["width"], 3), dtype=torch.float32, device="cuda") for _ in range(3)]
+    outs = [torch.empty((cfg.shard_rows(), c["width"], 3), dtype=torch.float32, device="cuda") for _ in range(max(DEPTHS))]
     res = {}
-    for depth in (1, 2, 3):
+    for depth in DEPTHS:
         for rep in range(2):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
