@@ -397,10 +397,10 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
 }
 
 template <typename Kern>
-static int persistent_grid(vpt_context* ctx, Kern kern, int* blocks)
+static int persistent_grid(vpt_context* ctx, Kern kern, int* blocks, int threads = 256)
 {
     int per_cu = 0, cus = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0));
     HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     if (per_cu < 1) per_cu = 1;
     *blocks = per_cu * cus;
@@ -482,7 +482,7 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         Q.partials = ctx->d_partials;
         Q.queue = ctx->d_queue;
         const Medium m{K.sigma_a, K.sigma_s, K.g, K.max_depth, K.march_step, K.march_light};
-        rc = persistent_grid(ctx, pool_kernel<EST, COUNT>, &blocks);
+        rc = persistent_grid(ctx, pool_kernel<EST, COUNT>, &blocks, VPT_POOL_THREADS);
         if (rc) return rc;
         const uint64_t need = (units + POOL - 1) / POOL;
         if ((uint64_t)blocks > need) blocks = (int)need;
@@ -494,7 +494,7 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
             HIP_OK(hipMemsetAsync(g_pool_stats + TL0, 0xFF, 3 * TL_MAXWG * sizeof(unsigned long long), stream));
             stats = g_pool_stats;
         }
-        pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(Q, m, S, K.counters, stats);
+        pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(VPT_POOL_THREADS), 0, stream>>>(Q, m, S, K.counters, stats);
         HIP_OK(hipGetLastError());
         const size_t npix = (size_t)K.shard_rows * (size_t)K.w;
         reduce_kernel<FB><<<dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream>>>(Q, K.out);

@@ -16,7 +16,7 @@
  * A wave takes the workgroup's ticket lock, returns its finished tasks to the rings of their next
  * stage, takes up to 64 tasks of the fullest ring, releases the lock, loads those states, runs
  * that ONE stage with (nearly) every lane busy, and stores the states back.  The pool is larger
- * than the workgroup (POOL > 256), so there is nearly always a full batch of some ring.
+ * than the workgroup (880 tasks for 512 lanes), so there is nearly always a full batch of some ring.
  *
  * Determinism: a task runs its unit's samples strictly in order and adds each sample to the
  * chunk sum as the reference adds to its pixel (acc = L + acc, src/rt.cpp:794); chunk sums are
@@ -35,11 +35,17 @@ namespace vpt {
 #ifndef VPT_POOL_DEBUG
 #define VPT_POOL_DEBUG 0
 #endif
+/* One 512-thread workgroup per CU (8 waves = 2 per SIMD) sharing one pool of 880 tasks (161 KB of
+ * LDS), vs two 256-thread workgroups of 440 each: A/B 46.48 -> 46.01 ms at 1024^2 x 256, 1/8 shard
+ * 6.76 -> 6.47 ms (more tasks per ring, fuller batches, half the unit rings to drain at the end). */
+#ifndef VPT_POOL_THREADS
+#define VPT_POOL_THREADS 512  /* threads per workgroup: its waves share one task pool */
+#endif
 #ifndef VPT_POOL_WGS
-#define VPT_POOL_WGS 2      /* workgroups per CU (occupancy target; LDS and VGPR budgets follow) */
+#define VPT_POOL_WGS 1      /* workgroups per CU (occupancy target; LDS and VGPR budgets follow) */
 #endif
 #ifndef VPT_POOL_SIZE
-#define VPT_POOL_SIZE 440
+#define VPT_POOL_SIZE 880
 #endif
 #ifndef VPT_SCHED_PRIO
 #define VPT_SCHED_PRIO 3    /* s_setprio level of the scheduler's critical section (0: off; A/B 3 vs 0: +0.7 %) */
@@ -56,11 +62,14 @@ namespace vpt {
 #ifndef VPT_PREP_ROUNDS
 #define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s) */
 #endif
-constexpr int POOL = VPT_POOL_SIZE;  /* task slots per workgroup (256 lanes): 81 KB of LDS at 440 */
+constexpr int POOL = VPT_POOL_SIZE;  /* task slots per workgroup: 182 B each + ~1.1 KB (161 KB at 880) */
 constexpr int NF = 18;      /* doubles per task */
 constexpr int NR = 7;       /* rings */
 constexpr int R_A = 0, R_S = 1, R_M = 5, R_DONE = NR;
-constexpr int URING = 256, UREFILL = 128;  /* work-unit ring: one global queue atomic per 128 units */
+#ifndef VPT_UREFILL
+#define VPT_UREFILL 128
+#endif
+constexpr int UREFILL = VPT_UREFILL, URING = 2 * UREFILL;  /* work-unit ring: one global queue atomic per UREFILL units */
 
 /* debug statistics, in builds with -DVPT_POOL_DEBUG=1 (=2: top-level cycle split only, cheaper;
  * scripts/build_variant.sh) run with
@@ -110,7 +119,7 @@ constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_
  * whose lap tags are current (written), and claims exactly that prefix with one CAS on the head.
  * An entry is read before the claim, and its position cannot be reserved again before the claim
  * (tail - head < POOL), so a claimed entry is never a later lap's. */
-constexpr int SLOT_BITS = 9, SLOT_MASK = (1 << SLOT_BITS) - 1, LAP_MASK = 127;
+constexpr int SLOT_BITS = POOL > 512 ? 10 : 9, SLOT_MASK = (1 << SLOT_BITS) - 1, LAP_MASK = (1 << (16 - SLOT_BITS)) - 1;
 static_assert(POOL <= (1 << SLOT_BITS), "slot ids must fit the ring entry");
 __device__ __forceinline__ uint16_t ring_entry(int slot, int pos)
 {
@@ -387,13 +396,13 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
 }
 
 template <int EST, bool COUNT>
-__global__ __launch_bounds__(256, VPT_POOL_WGS) void pool_kernel(PoolParams P, Medium m, const DevScene* __restrict__ S,
+__global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(PoolParams P, Medium m, const DevScene* __restrict__ S,
                                                    unsigned long long* counters, unsigned long long* stats)
 {
     __shared__ TaskPool sh;
     const int tid = threadIdx.x, lane = tid & 63;
     const uint64_t below = (1ull << lane) - 1ull;
-    for (int j = tid; j < POOL; j += 256) {
+    for (int j = tid; j < POOL; j += VPT_POOL_THREADS) {
         sh.c1[j] = 0;
         sh.samp[j] = 0;
         sh.evw[j] = 0;
