@@ -283,7 +283,7 @@ VPT_DEV double transmitance(dv3 a, dv3 b, double sigma_t)
 {
     dv3 aux = sub(b, a);
     double d = vm_sqrt(dot(aux, aux));
-    return vm_exp(sigma_t * d * -1.0);
+    return lm_exp(sigma_t * d * -1.0);
 }
 
 /* multipleT, include/volumetricBasicFunctions.h:26-57 (material-3 spheres only) */
@@ -305,8 +305,8 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
             tb = -b + sq;
             ta = -b - sq;
         }
-        if (tb < 0) T = T * vm_exp(-sigma_t * ta);
-        if (tb - ta > 0) T = T * vm_exp(-sigma_t * (tb - ta));
+        if (tb < 0) T = T * lm_exp(-sigma_t * ta);
+        if (tb - ta > 0) T = T * lm_exp(-sigma_t * (tb - ta));
     }
     return T;
 }
@@ -317,8 +317,8 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
 VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
 {
     double st, ct, sp, cp;
-    vm_sincos_acos(c, &st, &ct);
-    vm_sincos(phi, &sp, &cp);
+    lm_sincos_acos(c, &st, &ct);
+    lm_sincos(phi, &sp, &cp);
     return nrm(from_local(n, st * cp, st * sp, ct));
 }
 
@@ -357,8 +357,8 @@ VPT_DEV dv3 phase_sample(Sampler<COUNT>& smp, dv3 din)
     if (g == 0.0) {
         double phi = 2 * VPT_PI * xi2;
         double st, ct, sp, cp;
-        vm_sincos_acos(1 - 2 * xi1, &st, &ct);  /* theta = acos(1 - 2 xi1) */
-        vm_sincos(phi, &sp, &cp);
+        lm_sincos_acos(1 - 2 * xi1, &st, &ct);  /* theta = acos(1 - 2 xi1) */
+        lm_sincos(phi, &sp, &cp);
         return nrm(mk(st * cp, st * sp, ct));
     }
     double sq = (1.0 - g * g) / (1.0 - g + 2.0 * g * xi1);
@@ -367,7 +367,7 @@ VPT_DEV dv3 phase_sample(Sampler<COUNT>& smp, dv3 din)
     double st = st2 > 0.0 ? vm_sqrt(st2) : 0.0;
     double phi = 2 * VPT_PI * xi2;
     double sp, cp;
-    vm_sincos(phi, &sp, &cp);
+    lm_sincos(phi, &sp, &cp);
     return nrm(from_local(din, st * cp, st * sp, ct));
 }
 
@@ -409,7 +409,7 @@ VPT_DEV double ndf(double cosine, double alpha)
         double sine = vm_sqrt(1 - cosine * cosine);
         double fac1 = VPT_PI * alpha * alpha * cosine * cosine * cosine * cosine;
         double tang = sine / cosine;
-        double fac2 = vm_exp((-1 * tang * tang) / (alpha * alpha));
+        double fac2 = lm_exp((-1 * tang * tang) / (alpha * alpha));
         return (1 / fac1) * fac2;
     }
     return 0;
@@ -436,11 +436,11 @@ VPT_DEV double g1(dv3 n, dv3 wv, dv3 wh, double alpha)
 template <bool COUNT>
 VPT_DEV dv3 vector_facet(Sampler<COUNT>& smp, double alpha)
 {
-    double theta = vm_atan(vm_sqrt(-alpha * alpha * vm_log(1 - smp.next())));
+    double theta = lm_atan(vm_sqrt(-alpha * alpha * lm_log(1 - smp.next())));
     double phi = 2 * VPT_PI * smp.next();
     double st, ct, sp, cp;
-    vm_sincos(theta, &st, &ct);
-    vm_sincos(phi, &sp, &cp);
+    lm_sincos(theta, &st, &ct);
+    lm_sincos(phi, &sp, &cp);
     return nrm(mk(st * cp, st * sp, ct));
 }
 
@@ -938,7 +938,7 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     scene_isect(S, smp, xt, wl, tdist, idHit, false);
     if (src == idHit) {
         if (point) smp.tests(S->n);  /* the shadow ray the reference casts first (result overwritten) */
-        double it = vm_exp(sigma_t * tdist * -1.0);
+        double it = lm_exp(sigma_t * tdist * -1.0);
         double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, wl);
         dv3 Ls = scl(scl(rad, it), ph);
         if (with_sigma) Ld = scl(scl(scl(scl(Ls, trxt), sigma_s), (1 / prob_wl)), (1 / probSource));
@@ -965,10 +965,10 @@ VPT_DEV double equiangular_params2(const DevScene* __restrict__ S, Sampler<COUNT
     double dvn = vm_sqrt(dot(dv, dv));
     double proj = dot(dv, rd) / dot(rd, rd);
     D = vm_sqrt(dvn * dvn - proj * proj);
-    ta = vm_atan2(0.0 - proj, D);
-    tb = vm_atan2(tMax - proj, D);
+    ta = lm_atan2(0.0 - proj, D);
+    tb = lm_atan2(tMax - proj, D);
     double x = smp.next();
-    sample_t = D * vm_tan((1 - x) * ta + x * tb);
+    sample_t = D * lm_tan((1 - x) * ta + x * tb);
     return sample_t + proj;
 }
 
@@ -1047,8 +1047,8 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
     if (EST == 3) {  /* implicit: no light pick; success pdf freeFlightProb(d) * (1 - Tr(x, xs)) */
         const double TrActual = hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0;
         e.src = 0;
-        e.dist = -vm_log(1 - smp.next()) / sigma_t;
-        e.pdf = (sigma_t * vm_exp(sigma_t * e.dist * -1.0)) * (1.0 - TrActual);  /* :977 */
+        e.dist = -lm_log(1 - smp.next()) / sigma_t;
+        e.pdf = (sigma_t * lm_exp(sigma_t * e.dist * -1.0)) * (1.0 - TrActual);  /* :977 */
         if (!(e.dist > t)) return EV_MED;
         if (S->geo[id].emitter) {  /* :978-980: a light returns its radiance at any depth */
             p.L = add(p.L, mul(p.beta, sph_rad(S, id)));
@@ -1061,12 +1061,12 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
     e.src = S->emit[(int)(smp.next() * count)];
     bool surf;
     if (est_free_flight<EST>()) {
-        e.dist = -vm_log(1 - smp.next()) / sigma_t;  /* freeFlightSample, vptSamplingFunctions.h:11-14 */
+        e.dist = -lm_log(1 - smp.next()) / sigma_t;  /* freeFlightSample, vptSamplingFunctions.h:11-14 */
         surf = e.dist > t;
     } else {
         double D = 0, ta = 0, tb = 0, sd = 0;
         /* MIS: psurf = exp(-σt t) (:1419); explicit: TrActual = Tr(x, xs), 0 on a miss (:1033-1041) */
-        const double psurf = EST == 1 ? vm_exp(sigma_t * t * -1.0)
+        const double psurf = EST == 1 ? lm_exp(sigma_t * t * -1.0)
                                       : (hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0);
         e.dist = equiangular_params2(S, smp, e.src, t, p.o, p.d, D, ta, tb, sd);
         e.pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);

@@ -277,18 +277,18 @@ __global__ void math_probe_kernel(int fn, const double* x, const double* y, doub
     double a = x[i], b = y[i], r = 0;
     switch (fn) {
     case 0: r = vm_sqrt(a); break;
-    case 1: r = vm_exp(a); break;
-    case 2: r = vm_log(a); break;
-    case 3: r = vm_sin(a); break;
-    case 4: r = vm_cos(a); break;
-    case 5: r = vm_tan(a); break;
-    case 6: r = vm_atan(a); break;
-    case 7: r = vm_acos(a); break;
-    case 8: r = vm_atan2(a, b); break;
+    case 1: r = lm_exp(a); break;
+    case 2: r = lm_log(a); break;
+    case 3: r = lm_sin(a); break;
+    case 4: r = lm_cos(a); break;
+    case 5: r = lm_tan(a); break;
+    case 6: r = lm_atan(a); break;
+    case 7: r = lm_acos(a); break;
+    case 8: r = lm_atan2(a, b); break;
     case 10:
     case 11: {
         double sv, cv;
-        vm_sincos_acos(a, &sv, &cv);
+        lm_sincos_acos(a, &sv, &cv);
         r = fn == 10 ? sv : cv;
         break;
     }

@@ -66,11 +66,14 @@ def prims():
     return dict(np.load(os.path.join(GOLDEN, "primitives.npz")))
 
 
-@pytest.fixture(scope="session")
-def orc():
+@pytest.fixture(scope="session", params=["libm", "portable"])
+def orc(request):
+    """both oracle builds: libm (glibc calls) and portable (csrc/vpt_math.h lm_*, the HIP kernel's
+    arithmetic).  With VPT_GLIBC_MATH=1 the two are the same function bit for bit, so every
+    reference bar holds for the arithmetic the GPU executes."""
     from oracle.oracle import Oracle
 
-    return Oracle(portable=False)
+    return Oracle(portable=request.param == "portable")
 
 
 @pytest.fixture(scope="session")
