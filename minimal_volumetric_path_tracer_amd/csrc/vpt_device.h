@@ -312,13 +312,12 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
 }
 
 /* ------------------------------------------------------------------ sampling */
-/* direction at polar angle theta = acos(c) and azimuth phi around n; sin/cos of the acos as the
- * build's libm evaluates them (vm_sincos_acos) */
+/* direction at polar angle theta = acos(c) and azimuth phi around n: the reference computes
+ * sin(acos c), cos(acos c), sin(phi), cos(phi) with libm (lm_dir_trig, bit for bit) */
 VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
 {
     double st, ct, sp, cp;
-    lm_sincos_acos(c, &st, &ct);
-    lm_sincos(phi, &sp, &cp);
+    lm_dir_trig(c, phi, &st, &ct, &sp, &cp);
     return nrm(from_local(n, st * cp, st * sp, ct));
 }
 
@@ -357,8 +356,7 @@ VPT_DEV dv3 phase_sample(Sampler<COUNT>& smp, dv3 din)
     if (g == 0.0) {
         double phi = 2 * VPT_PI * xi2;
         double st, ct, sp, cp;
-        lm_sincos_acos(1 - 2 * xi1, &st, &ct);  /* theta = acos(1 - 2 xi1) */
-        lm_sincos(phi, &sp, &cp);
+        lm_dir_trig(1 - 2 * xi1, phi, &st, &ct, &sp, &cp);  /* theta = acos(1 - 2 xi1) */
         return nrm(mk(st * cp, st * sp, ct));
     }
     double sq = (1.0 - g * g) / (1.0 - g + 2.0 * g * xi1);
@@ -439,8 +437,7 @@ VPT_DEV dv3 vector_facet(Sampler<COUNT>& smp, double alpha)
     double theta = lm_atan(vm_sqrt(-alpha * alpha * lm_log(1 - smp.next())));
     double phi = 2 * VPT_PI * smp.next();
     double st, ct, sp, cp;
-    lm_sincos(theta, &st, &ct);
-    lm_sincos(phi, &sp, &cp);
+    lm_sincos2(theta, phi, &st, &ct, &sp, &cp);
     return nrm(mk(st * cp, st * sp, ct));
 }
 

@@ -29,7 +29,7 @@ run() {  # run <name> <seconds> <cmd...>
 
 for s in $STEPS; do
     case $s in
-        tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py --steps 3 --warmup 1 ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- \

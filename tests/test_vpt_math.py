@@ -1,6 +1,7 @@
-"""The build's portable FP64 libm (csrc/vpt_math.h, evaluated on the host through the oracle's
-portable build) against glibc: every function within 3 ulp over the argument ranges the tracer
-uses, special values handled like C99 Annex F."""
+"""The path's libm as the oracle's portable build evaluates it (lm_* of csrc/vpt_math.h: the
+glibc-exact restatement of csrc/vpt_glibm.h, the same source the kernel compiles) against the
+host's glibc: within 3 ulp everywhere on the tracer's ranges (tests/test_glibc_libm.py holds the
+bit-exact bar), special values handled like C99 Annex F."""
 import numpy as np
 import pytest
 
@@ -58,23 +59,3 @@ def test_special_values(orc, orc_vm):
     assert orc_vm.math(1, np.array([0.0]))[0] == 1.0
     s = orc_vm.math(3, np.array([0.0]))[0]
     assert s == 0.0 and orc_vm.math(4, np.array([0.0]))[0] == 1.0
-
-
-def test_sincos_acos_vs_exact(orc, orc_vm):
-    """sin(acos c), cos(acos c) -- the build's libm evaluates them as sqrt((1-c)(1+c)) and c
-    (csrc/vpt_math.h vm_sincos_acos): within 1 ulp of the exact values (200-bit mpmath).  glibc's
-    composition of two rounded functions (what the reference computes) is itself up to ~50 ulp off
-    for sin and thousands of ulp for cos(acos c) at small c, so the bar is against the exact value."""
-    mpmath = pytest.importorskip("mpmath")
-    mpmath.mp.prec = 200
-    rng = np.random.default_rng(10)
-    c = np.concatenate([rng.uniform(-1, 1, 2000), rng.uniform(0.999, 1, 500), rng.uniform(-1, -0.999, 500),
-                        [-1.0, 1.0, 0.0, -0.0, 0.5, -0.5, 1e-300]])
-    s = orc_vm.math(10, c)
-    ex = np.array([float(mpmath.sqrt((1 - mpmath.mpf(x)) * (1 + mpmath.mpf(x)))) for x in c])  # = sin(acos c), exact
-    assert ulps(s, ex).max() <= 1
-    assert np.array_equal(orc_vm.math(11, c), c)
-    # away from c = -1 (where glibc's pi - acos cancels) and tiny c, glibc agrees to a few ulp
-    m = (c > -0.9) & (np.abs(c) > 1e-3)
-    assert ulps(s[m], orc.math(10, c[m])).max() <= 4
-    assert np.isnan(orc_vm.math(10, np.array([np.nan]))[0]) and np.isnan(orc_vm.math(10, np.array([1.5]))[0])
