@@ -139,7 +139,10 @@ int vpt_set_scene(vpt_context* ctx, const vpt_sphere* spheres, int n);
 
 /* Renders into a DEVICE buffer on `stream` (a hipStream_t, NULL = default stream); returns
  * after enqueueing.  d_out: vpt_shard_rows(p) * width * 3 elements of fb_format, the
- * per-pixel average BEFORE the clamp of src/rt.cpp:803. */
+ * per-pixel average BEFORE the clamp of src/rt.cpp:803.  Renders on different streams of one
+ * context may be in flight together: each stream gets its own work queue and partial-sum
+ * buffer (stream-ordered, grown on demand); calls on one stream run in order.  The scene must
+ * not change (vpt_set_scene) while a render that uses it is in flight. */
 int vpt_render_device(vpt_context* ctx, const vpt_params* p, void* d_out, void* stream);
 
 /* Same, synchronous, host output buffer. */

@@ -13,6 +13,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <vector>
+
 #include "vpt_device.h"
 #include "vpt_pool.h"
 #include "vpt_internal.h"
@@ -303,16 +306,51 @@ unsigned long long* g_pool_stats = nullptr;  /* debug statistics buffer (VPT_POO
 
 }  // namespace
 
+/* Per-stream launch state: a render enqueued on one stream must not share its work queue or its
+ * chunk partials with a render in flight on another stream of the same context.  Each stream
+ * that renders gets its own slot (queue head + partials, grown on demand, stream-ordered), so
+ * vpt_render_device may be called on several streams of one context at once. */
+struct StreamSlot {
+    hipStream_t stream;
+    unsigned* d_queue;
+    double* d_partials;      /* chunk sums of the pool kernel */
+    size_t partials_bytes;
+};
+
 struct vpt_context {
     int device;
     DevScene* d_scene;
     DevScene h_scene;
     int has_scene;
     unsigned long long* d_counters;
-    unsigned* d_queue;
-    double* d_partials;      /* chunk sums of the pool kernel, grown on demand */
-    size_t partials_bytes;
+    std::mutex mu;           /* guards slots */
+    std::vector<StreamSlot> slots;
 };
+
+/* the stream's slot, created on first use; partials grown to `pbytes` in stream order (the
+ * previous buffer is freed after the work already queued on the stream) */
+static int stream_slot(vpt_context* ctx, hipStream_t stream, size_t pbytes, StreamSlot** out)
+{
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    StreamSlot* sl = nullptr;
+    for (auto& x : ctx->slots)
+        if (x.stream == stream) sl = &x;
+    if (!sl) {
+        StreamSlot n{stream, nullptr, nullptr, 0};
+        HIP_OK(hipMalloc((void**)&n.d_queue, sizeof(unsigned)));
+        ctx->slots.push_back(n);
+        sl = &ctx->slots.back();
+    }
+    if (pbytes > sl->partials_bytes) {
+        if (sl->d_partials) HIP_OK(hipFreeAsync(sl->d_partials, stream));
+        sl->d_partials = nullptr;
+        sl->partials_bytes = 0;
+        HIP_OK(hipMallocAsync((void**)&sl->d_partials, pbytes, stream));
+        sl->partials_bytes = pbytes;
+    }
+    *out = sl;
+    return VPT_OK;
+}
 
 static int check_medium(const vpt_medium* m)
 {
@@ -407,8 +445,16 @@ static int persistent_grid(vpt_context* ctx, Kern kern, int* blocks, int threads
     return VPT_OK;
 }
 
+/* A/B and debug switches read from the environment (VPT_SIMPLE_KERNEL, VPT_WAVE_KERNEL,
+ * VPT_COST_SURF / VPT_COST_MED, VPT_POOL_STATS) exist only in builds made with -DVPT_DEBUG_ENV=1
+ * (scripts/build_variant.sh); the production library ignores the environment, so a stray
+ * variable cannot change the kernel or its timing. */
+#ifndef VPT_DEBUG_ENV
+#define VPT_DEBUG_ENV 0
+#endif
 static int env_int(const char* name, int dflt)
 {
+    if (!VPT_DEBUG_ENV) return dflt;
     const char* v = getenv(name);
     return (v && *v) ? atoi(v) : dflt;
 }
@@ -463,7 +509,6 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         Q.level_units = (unsigned)K.tiles_x * (unsigned)K.tiles_y * 64u;
         const uint64_t units = (uint64_t)K.tiles_x * (uint64_t)K.tiles_y * 64u * (uint64_t)Q.nch;
         if (units >= 0xFFFFFFFFull) return vpt_fail(VPT_E_INVALID, "too many work units (%llu)", (unsigned long long)units);
-        Q.nunits = (unsigned)units;
         Q.seed = K.seed;
         for (int i = 0; i < 3; ++i) {
             Q.o[i] = K.o[i];
@@ -472,21 +517,23 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
             Q.cy[i] = K.cy[i];
         }
         const size_t pbytes = (size_t)K.shard_rows * (size_t)K.w * (size_t)Q.nch * 3 * sizeof(double);
-        if (pbytes > ctx->partials_bytes) {
-            if (ctx->d_partials) HIP_OK(hipFree(ctx->d_partials));
-            ctx->d_partials = nullptr;
-            ctx->partials_bytes = 0;
-            HIP_OK(hipMalloc((void**)&ctx->d_partials, pbytes));
-            ctx->partials_bytes = pbytes;
-        }
-        Q.partials = ctx->d_partials;
-        Q.queue = ctx->d_queue;
+        StreamSlot* sl = nullptr;
+        rc = stream_slot(ctx, stream, pbytes, &sl);
+        if (rc) return rc;
+        Q.partials = sl->d_partials;
+        Q.queue = sl->d_queue;
         const Medium m{K.sigma_a, K.sigma_s, K.g, K.max_depth, K.march_step, K.march_light};
         rc = persistent_grid(ctx, pool_kernel<EST, COUNT>, &blocks, VPT_POOL_THREADS);
         if (rc) return rc;
         const uint64_t need = (units + POOL - 1) / POOL;
         if ((uint64_t)blocks > need) blocks = (int)need;
-        HIP_OK(hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned), stream));
+        /* every workgroup adds UREFILL to the u32 queue once more after it runs dry */
+        if (units + (uint64_t)blocks * (UREFILL + 1) >= 0xFFFFFFFFull)
+            return vpt_fail(VPT_E_INVALID, "too many work units (%llu) for the u32 work queue", (unsigned long long)units);
+        /* The pool's ring positions are 32-bit counters that grow by ~3 per sample a workgroup
+         * runs: launches are capped at 2^26 samples per workgroup (units in order, one partial
+         * slot each, so splitting changes no value); one launch up to ~17 G samples on 256 CUs. */
+        const uint64_t max_units = (((uint64_t)1 << 26) * (uint64_t)blocks) / (uint64_t)(K.chunk > 0 ? K.chunk : 1);
         unsigned long long* stats = nullptr;
         if (env_int("VPT_POOL_STATS", 0)) {  /* debug: scheduler statistics, vpt_debug_pool_stats */
             if (!g_pool_stats) HIP_OK(hipMalloc((void**)&g_pool_stats, (TL0 + 3 * TL_MAXWG) * sizeof(unsigned long long)));
@@ -494,8 +541,13 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
             HIP_OK(hipMemsetAsync(g_pool_stats + TL0, 0xFF, 3 * TL_MAXWG * sizeof(unsigned long long), stream));
             stats = g_pool_stats;
         }
-        pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(VPT_POOL_THREADS), 0, stream>>>(Q, m, S, K.counters, stats);
-        HIP_OK(hipGetLastError());
+        for (uint64_t u0 = 0; u0 < units; u0 += max_units) {
+            Q.unit0 = (unsigned)u0;
+            Q.nunits = (unsigned)(units - u0 < max_units ? units - u0 : max_units);
+            HIP_OK(hipMemsetAsync(Q.queue, 0, sizeof(unsigned), stream));
+            pool_kernel<EST, COUNT><<<dim3((unsigned)blocks), dim3(VPT_POOL_THREADS), 0, stream>>>(Q, m, S, K.counters, stats);
+            HIP_OK(hipGetLastError());
+        }
         const size_t npix = (size_t)K.shard_rows * (size_t)K.w;
         reduce_kernel<FB><<<dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream>>>(Q, K.out);
         HIP_OK(hipGetLastError());
@@ -516,8 +568,11 @@ static int launch_wave(vpt_context* ctx, KParams K, hipStream_t stream)
     const int need = (tiles + 3) / 4;  /* 4 waves per block, one tile per wave to start */
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
-    K.queue = ctx->d_queue;
-    HIP_OK(hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned), stream));
+    StreamSlot* sl = nullptr;
+    rc = stream_slot(ctx, stream, 0, &sl);
+    if (rc) return rc;
+    K.queue = sl->d_queue;
+    HIP_OK(hipMemsetAsync(K.queue, 0, sizeof(unsigned), stream));
     render_kernel<EST, COUNT, FB><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(K, S);
     HIP_OK(hipGetLastError());
     return VPT_OK;
@@ -565,12 +620,8 @@ int vpt_context_create(int device, vpt_context** out)
     c->has_scene = 0;
     c->d_scene = nullptr;
     c->d_counters = nullptr;
-    c->d_queue = nullptr;
-    c->d_partials = nullptr;
-    c->partials_bytes = 0;
     hipError_t e = hipMalloc((void**)&c->d_scene, sizeof(DevScene));
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long));
-    if (e == hipSuccess) c->d_queue = (unsigned*)(c->d_counters + 2);
     if (e != hipSuccess) {
         vpt_context_destroy(c);
         return vpt_fail(VPT_E_HIP, "vpt_context_create: hipMalloc: %s", hipGetErrorString(e));
@@ -587,7 +638,10 @@ void vpt_context_destroy(vpt_context* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->d_scene) (void)hipFree(ctx->d_scene);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
-    if (ctx->d_partials) (void)hipFree(ctx->d_partials);
+    for (auto& sl : ctx->slots) {
+        if (sl.d_partials) (void)hipFree(sl.d_partials);
+        if (sl.d_queue) (void)hipFree(sl.d_queue);
+    }
     (void)hipSetDevice(prev);
     delete ctx;
 }

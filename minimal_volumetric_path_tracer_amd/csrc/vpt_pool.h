@@ -66,10 +66,16 @@ constexpr int POOL = VPT_POOL_SIZE;  /* task slots per workgroup: 182 B each + ~
 constexpr int NF = 18;      /* doubles per task */
 constexpr int NR = 7;       /* rings */
 constexpr int R_A = 0, R_S = 1, R_M = 5, R_DONE = NR;
+/* the scheduler's counters (TaskPool::ctl): ring tails, ring heads, slots retired, the unit ring's
+ * tail, queue exhausted, refill in progress */
+constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_EXH = 2 * NR + 2, C_RFL = 2 * NR + 3,
+              NCTL = 2 * NR + 4;
+static_assert(NCTL <= 64, "the counters are read lane-parallel by one wave");
 #ifndef VPT_UREFILL
 #define VPT_UREFILL 128
 #endif
 constexpr int UREFILL = VPT_UREFILL, URING = 2 * UREFILL;  /* work-unit ring: one global queue atomic per UREFILL units */
+static_assert(URING >= 2 * UREFILL, "a refill (at most UREFILL entries from utail < uhead + UREFILL) must stay below uhead + URING");
 
 /* debug statistics, in builds with -DVPT_POOL_DEBUG=1 (=2: top-level cycle split only, cheaper;
  * scripts/build_variant.sh) run with
@@ -105,13 +111,11 @@ struct TaskPool {
     uint16_t ring[NR][POOL]; /* slots waiting, per ring */
     /* the scheduler's counters, contiguous so that one lane-parallel LDS read fetches them all:
      * monotonic ring tails and heads, slots retired, the unit ring's tail, queue exhausted */
-    int ctl[2 * NR + 3];
+    int ctl[NCTL];
     int ticket, serving;     /* FIFO ticket lock: a wave returning tasks is never starved */
     uint32_t uring[URING];   /* prefetched work units (refilled under the lock, taken by CAS on uhead) */
     int uhead;
 };
-constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_EXH = 2 * NR + 2, C_RFL = 2 * NR + 3,
-              NCTL = 2 * NR + 4;
 
 /* Lock-free rings (VPT_LOCKFREE): an entry is the slot and the lap of its ring position,
  * slot | (position / POOL mod 128) << 9.  A producer reserves positions with one atomic add on the
@@ -137,7 +141,8 @@ struct PoolParams {
     int tiles_x, nch;
     vpt_chunk_layout lay;   /* chunks of a pixel's samples (vpt_chunks.h) */
     unsigned level_units;   /* units per chunk index: 64 pixels x tiles */
-    unsigned nunits;
+    unsigned nunits;        /* units of this launch: unit0, unit0 + 1, ... */
+    unsigned unit0;
     uint64_t seed;
     double o[3], d[3], cx[3], cy[3];
     double* partials;       /* nch * rows * w * 3: chunk-major, so the units of one chunk level (handed
@@ -156,6 +161,7 @@ struct Unit {
 
 __device__ __forceinline__ Unit decode_unit(const PoolParams& P, unsigned u)
 {
+    u += P.unit0;
     Unit r;
     const unsigned c = u / P.level_units, rem = u - c * P.level_units;
     r.c = (int)c;
@@ -287,36 +293,43 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         if (needm) {
             const int leader = __ffsll((unsigned long long)needm) - 1;
             const int k = __popcll(needm);
+            const int r = __popcll(needm & below);
             int h = 0, got = 0, ex = 0;
-            if (lane == leader) {  /* take up to k units from the workgroup's ring */
-                ex = __hip_atomic_load(&sh.ctl[C_EXH], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                h = lds_peek(&sh.uhead);
-                while (true) {
+            uint32_t ent = 0;
+            /* take up to k units from the workgroup's ring: read the entries, then claim exactly
+             * them with one CAS on uhead.  Reading before the claim keeps a refill from reusing
+             * the entries' positions under a reader: a refill writes below uhead + 2 UREFILL =
+             * uhead + URING, and uhead stays h until this CAS succeeds. */
+            while (true) {
+                if (lane == leader) {
+                    ex = __hip_atomic_load(&sh.ctl[C_EXH], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    h = lds_peek(&sh.uhead);
                     const int avail =
                         __hip_atomic_load(&sh.ctl[C_UTAIL], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - h;
-                    got = min(k, avail);
-                    if (got <= 0) {
-                        got = 0;
-                        break;
-                    }
-                    if (__hip_atomic_compare_exchange_strong(&sh.uhead, &h, h + got, __ATOMIC_ACQUIRE,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-                        break;
+                    got = max(0, min(k, avail));
                 }
+                h = __shfl(h, leader);
+                got = __shfl(got, leader);
+                ex = __shfl(ex, leader);
+                if (need && r < got) ent = ((volatile uint32_t*)sh.uring)[(h + r) % URING];
+                if (got == 0) break;
+                int won = 0;
+                if (lane == leader) {
+                    int hh = h;
+                    won = __hip_atomic_compare_exchange_strong(&sh.uhead, &hh, h + got, __ATOMIC_RELAXED,
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                if (__shfl(won, leader)) break;
             }
-            h = __shfl(h, leader);
-            got = __shfl(got, leader);
-            ex = __shfl(ex, leader);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (need) {
-                const int r = __popcll(needm & below);
                 if (r >= got) {
                     /* ring empty: retire only once the queue is exhausted (the flag was read before
                      * utail, so no unit can still be on its way in); otherwise back to ring A */
                     if (ex) done = true;
                     else parked = true;
                 } else {
-                    const Unit uu = decode_unit(P, sh.uring[(h + r) % URING]);
+                    const Unit uu = decode_unit(P, ent);
                     if (uu.valid) {  /* (an invalid unit -- a tile's padding -- is dropped) */
                         t.pix = (unsigned)uu.x | ((unsigned)uu.y << 16);
                         t.key = vpt_stream_key(P.seed, (uint64_t)(P.h - 1 - uu.y) * (uint64_t)P.w + (uint64_t)uu.x);

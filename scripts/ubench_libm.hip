@@ -18,8 +18,8 @@ __device__ __forceinline__ double u01(unsigned long long& s)
     return (double)(s >> 11) * 0x1p-53;
 }
 
-enum { F_EXP, F_LOG, F_SIN, F_COS, F_SINCOS, F_TAN, F_ATAN2, F_ACOS, F_SCACOS, F_ATAN, NF };
-static const char* NAMES[NF] = {"exp", "log", "sin", "cos", "sincos", "tan", "atan2", "acos", "sincos_acos", "atan"};
+enum { F_EXP, F_LOG, F_SIN, F_COS, F_SINCOS, F_TAN, F_ATAN2, F_ACOS, F_SCACOS, F_ATAN, F_DIR, F_DIRCONE, NF };
+static const char* NAMES[NF] = {"exp", "log", "sin", "cos", "sincos", "tan", "atan2", "acos", "sincos_acos", "atan", "dir_trig", "dir_cone"};
 
 template <int F, int IMPL>
 __global__ __launch_bounds__(256) void bench(double* out, int iters)
@@ -47,6 +47,16 @@ __global__ __launch_bounds__(256) void bench(double* out, int iters)
             if (IMPL) lm_sincos_acos(2.0 * u - 1.0, &a, &b);
             else vm_sincos_acos(2.0 * u - 1.0, &a, &b);
             r = a + b;
+        }
+        if (F == F_DIR || F == F_DIRCONE) {  /* lm_dir_trig: sin/cos of acos(c) and of phi */
+            const double c = F == F_DIR ? 2.0 * u - 1.0 : (1.0 - u) + u * 0.9998;
+            double a, b, e, f;
+            if (IMPL) lm_dir_trig(c, 6.283185307179586 * v, &a, &b, &e, &f);
+            else {
+                vm_sincos_acos(c, &a, &b);
+                vm_sincos(6.283185307179586 * v, &e, &f);
+            }
+            r = a * e + b * f;
         }
         if (F == F_ATAN) r = IMPL ? lm_atan(20.0 * u - 10.0) : vm_atan(20.0 * u - 10.0);
         acc += r;
@@ -78,10 +88,15 @@ static void row(double* d)
     printf("%-12s vm %8.2f Gcalls/s   lm %8.2f Gcalls/s   lm/vm %.2f\n", NAMES[F], vm, lm, lm / vm);
 }
 
-int main()
+int main(int argc, char** argv)
 {
     double* d;
     (void)hipMalloc(&d, sizeof(double) * 256 * 8 * 256);
+    if (argc > 1) {  /* one function only (for rocprofv3 --pmc): dir */
+        row<F_DIR>(d);
+        (void)hipFree(d);
+        return 0;
+    }
     row<F_EXP>(d);
     row<F_LOG>(d);
     row<F_SIN>(d);
@@ -92,6 +107,8 @@ int main()
     row<F_ACOS>(d);
     row<F_SCACOS>(d);
     row<F_ATAN>(d);
+    row<F_DIR>(d);
+    row<F_DIRCONE>(d);
     (void)hipFree(d);
     return 0;
 }
