@@ -12,7 +12,15 @@ them in flight, each on its own context and HIP stream, so that a launch's drain
 paths of its last samples, ~0.5 ms) and its gather overlap the next launch (--inflight 1: serialized).
 Inputs (the 1.4 KB scene) are resident in HBM before the timed region; nothing is skipped.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ff|mis|dense] [--no-cpu] [--inflight D]
+With --config ff (the default) the same run also measures BASELINE.json configs[2] -- MIS +
+HG g=0.5, 1024^2 x 1024 spp, the north-star workload -- and reports it in the line's "north_star"
+object next to the reference's MIS rate on this host (--no-north-star skips it).  The CPU leg
+(cpu_baseline, rank 0 at N=1) times the reference program itself, built from its own sources by
+oracle/Makefile: with a per-thread RNG (the fair flavour) and as written; and it checks sampled
+rows of the GPU image against the reference's own functions (rmse_vs_reference_per_channel).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ff|mis|dense|mis4k] [--no-cpu]
+                    [--no-north-star] [--inflight D]
 """
 from __future__ import annotations
 
@@ -38,14 +46,18 @@ METRIC = "Msamples/s (pixels×spp/s) at 1024²; per-channel RMSE vs CPU PPM"
 FLOP_PER_TEST = 20          # Sphere::intersect, include/Sphere.h:27-37
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector (= FP64 matrix) peak, spec
 BAND_ROWS = 16
+NORTH_STAR = "mis"          # BASELINE.json configs[2], measured beside the headline config
 
 CONFIGS = {
     # BASELINE.json configs[1]
     "ff": dict(width=1024, height=1024, spp=256, estimator="ff", sigma_a=0.001, sigma_s=0.009),
     # BASELINE.json configs[2] (HG g = 0.5 extension), reduced to fit a quick bench: 1024 spp
     "mis": dict(width=1024, height=1024, spp=1024, estimator="mis", sigma_a=0.001, sigma_s=0.009, hg_g=0.5),
-    # BASELINE.json configs[3]: dense medium, 8 bounces
-    "dense": dict(width=2048, height=2048, spp=4096, estimator="ff", sigma_a=0.01, sigma_s=0.09, max_depth=8),
+    # BASELINE.json configs[3]: dense medium, 8 bounces.  sigma_t 0.03 (3x the default, albedo 0.9 kept):
+    # at SURVEY's proposed 0.1 the ~180 units of fog between the camera (z = 214) and the scene pass
+    # exp(-18) = 1.5e-8 of the light and the image is black (mean 1.5e-8); at 0.03 the mean is 6 % of
+    # the default scene's and every pixel is lit
+    "dense": dict(width=2048, height=2048, spp=4096, estimator="ff", sigma_a=0.003, sigma_s=0.027, max_depth=8),
     # BASELINE.json configs[4]: meant for --gpus 8 (137 G samples per image; ~4 s per step on 8 GPUs)
     "mis4k": dict(width=4096, height=4096, spp=8192, estimator="mis", sigma_a=0.001, sigma_s=0.009),
 }
@@ -81,33 +93,120 @@ def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 12, band
             "rmse_vs_gpu_per_channel": [float(x) for x in np.sqrt(se / n)]}
 
 
-def cpu_baseline(threads: int) -> dict:
-    """The reference program itself (oracle/_ref/rt, built from /root/reference's sources by
-    oracle/Makefile) on this host's cores: `rt 32` = 1024x768x32 (25 M samples, ~13 s) with its racy
-    shared erand48 state, as written.  Msamples/s = w*h*spp / the elapsed time it prints
-    (src/rt.cpp:824-827, includes its serial PPM write).  Falls back to the oracle restatement."""
-    exe = os.path.join(ROOT, "oracle", "_ref", "rt")
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    if os.path.exists(exe):
-        spp = 32
-        with tempfile.TemporaryDirectory() as td:
-            r = subprocess.run([exe, str(spp)], cwd=td, capture_output=True, text=True, timeout=900, env=env)
-        m = re.search(r"elapsed time: ([0-9.eE+-]+)s", r.stdout)
-        if r.returncode == 0 and m:
-            el = float(m.group(1))
-            return {"value": 1024 * 768 * spp / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "reference",
-                    "sample": f"reference program src/rt.cpp as written (shared racy erand48 state), `rt {spp}` = "
-                              f"1024x768x{spp} spp free-flight, default scene, OpenMP {threads} threads, "
-                              f"elapsed {el:.2f}s incl. its PPM write"}
-    from oracle.oracle import Oracle  # cpu_baseline leg only
+def cpu_topology(threads: int) -> dict:
+    """The host's CPU model, socket 0's physical core count, and `threads` CPUs to pin the CPU
+    legs to: distinct physical cores of socket 0 (one hardware thread each) among the CPUs this
+    process may use.  On the GPU box the job's CPU share is 16 (OMP_NUM_THREADS), less than a socket."""
+    import glob
 
-    o = Oracle(portable=False)
-    o.set_scene(vpt.default_scene())
-    t = time.time()
-    o.render(1024, 256, 8, 0, threads=threads)
-    el = time.time() - t
-    return {"value": 1024 * 256 * 8 / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle restatement (per-sample streams), 1024x256x8 spp free-flight, {threads} threads"}
+    allowed = sorted(os.sched_getaffinity(0))
+    topo = {}
+    for d in glob.glob("/sys/devices/system/cpu/cpu[0-9]*"):
+        try:
+            cpu = int(d.rsplit("cpu", 1)[1])
+            pkg = int(open(os.path.join(d, "topology", "physical_package_id")).read())
+            core = int(open(os.path.join(d, "topology", "core_id")).read())
+        except (OSError, ValueError):
+            continue
+        topo[cpu] = (pkg, core)
+    pkg0 = topo[allowed[0]][0] if allowed and allowed[0] in topo else 0
+    socket_cores = len({c for (p, c) in topo.values() if p == pkg0}) or (os.cpu_count() or 1)
+    pick, seen = [], set()
+    for cpu in allowed:
+        pc = topo.get(cpu, (pkg0, cpu))
+        if pc[0] == pkg0 and pc[1] not in seen:
+            seen.add(pc[1])
+            pick.append(cpu)
+    if len(pick) < threads:  # not enough distinct cores on socket 0: fill with the other allowed CPUs
+        pick += [c for c in allowed if c not in pick]
+    model = ""
+    try:
+        m = re.search(r"model name\s*:\s*(.*)", open("/proc/cpuinfo").read())
+        model = m.group(1).strip() if m else ""
+    except OSError:
+        pass
+    return {"cpus": pick[:threads], "socket_physical_cores": socket_cores, "model": model}
+
+
+def run_reference_program(exe: str, spp: int, cpus: list) -> float:
+    """Runs `exe <spp>` (the reference's main, 1024 x 768, src/rt.cpp:752) pinned to `cpus` with one
+    OpenMP thread per CPU and returns the elapsed time it prints (src/rt.cpp:824-827; includes its
+    serial PPM write).  The affinity is set on this process around the spawn, so the child inherits it."""
+    saved = os.sched_getaffinity(0)
+    env = dict(os.environ, OMP_NUM_THREADS=str(len(cpus)), OMP_PROC_BIND="close")
+    try:
+        os.sched_setaffinity(0, cpus)
+        with tempfile.TemporaryDirectory() as td:
+            r = subprocess.run([exe, str(spp)], cwd=td, capture_output=True, text=True, timeout=300, env=env)
+    finally:
+        os.sched_setaffinity(0, saved)
+    m = re.search(r"elapsed time: ([0-9.eE+-]+)s", r.stdout)
+    if r.returncode != 0 or not m:
+        raise RuntimeError(f"{exe} {spp}: rc {r.returncode}: {r.stdout[-200:]} {r.stderr[-200:]}")
+    return float(m.group(1))
+
+
+def reference_rows_check(img: np.ndarray, c: dict, rows=(0, 1, 2, 3)) -> dict:
+    """Per-channel RMSE of the bench image's file rows `rows` (spread over the image) against the
+    reference's own functions (oracle/_ref/libvpt_ref.so: the reference headers compiled in place,
+    its pixel loop with the same per-sample erand48 streams), and that sample's single-core rate."""
+    from oracle.oracle import Reference  # cpu_baseline leg only
+
+    H, W, SPP = c["height"], c["width"], c["spp"]
+    est = {"ff": 0, "mis": 1}[c["estimator"]]
+    ref = Reference()
+    ref.set_scene(ref.default_scene())
+    se, n, el = np.zeros(3), 0, 0.0
+    for k in rows:
+        fr = (H - 1) * k // max(len(rows) - 1, 1)   # file row
+        y = H - 1 - fr                              # camera row
+        t = time.time()
+        out = ref.render(W, H, SPP, est, c["sigma_a"], c["sigma_s"], seed=0x5EED0001, y0=y, y1=y + 1)
+        el += time.time() - t
+        d = img[fr].astype(np.float64) - out[fr].astype(np.float32).astype(np.float64)
+        se += (d * d).sum(0)
+        n += W
+    return {"rmse_vs_reference_per_channel": [float(x) for x in np.sqrt(se / n)],
+            "reference_rows": f"file rows {[(H - 1) * k // max(len(rows) - 1, 1) for k in rows]} x {W} x {SPP} spp, "
+                              "oracle/_ref/libvpt_ref.so (the reference's own functions), one core",
+            "reference_one_core_msamples_s": len(rows) * W * SPP / el / 1e6}
+
+
+def cpu_baseline(img: np.ndarray, c: dict, threads: int) -> dict:
+    """The reference program on this host's cores, pinned to `threads` physical cores of socket 0:
+    oracle/_ref/rt_tls (src/rt.cpp with its erand48 state made per-thread, oracle/ref_tls_rng.h:
+    BASELINE.md's fair "per-thread RNG" flavour) at `threads` cores and at one core, and
+    oracle/_ref/rt (as written: one erand48 state shared by every thread).  Both are
+    built from /root/reference's sources by oracle/Makefile.  Samples are the program's own
+    1024 x 768 free-flight image at a reduced spp (~5-10 s each)."""
+    topo = cpu_topology(threads)
+    cpus = topo["cpus"]
+    tls, asis = os.path.join(ROOT, "oracle", "_ref", "rt_tls"), os.path.join(ROOT, "oracle", "_ref", "rt")
+    px = 1024 * 768
+    spp_n, spp_1, spp_a = 64, 4, 16
+    el_n = run_reference_program(tls, spp_n, cpus)
+    el_1 = run_reference_program(tls, spp_1, cpus[:1])
+    el_a = run_reference_program(asis, spp_a, cpus)
+    v_n, v_1, v_a = px * spp_n / el_n / 1e6, px * spp_1 / el_1 / 1e6, px * spp_a / el_a / 1e6
+    S = topo["socket_physical_cores"]
+    res = {
+        "value": v_n, "unit": "Msamples/s", "cores": len(cpus), "kind": "reference",
+        "sample": f"reference program src/rt.cpp with a per-thread erand48 state (oracle/_ref/rt_tls), "
+                  f"`rt_tls {spp_n}` = 1024x768x{spp_n} free-flight, default scene, {len(cpus)} OpenMP threads "
+                  f"pinned to {len(cpus)} physical cores of socket 0, elapsed {el_n:.2f}s incl. its PPM write",
+        "cpu_model": topo["model"],
+        "socket_physical_cores": S,
+        "one_core": {"value": v_1, "sample": f"rt_tls {spp_1}, 1 thread, {el_1:.2f}s"},
+        "parallel_efficiency": v_n / (v_1 * len(cpus)),
+        "socket_estimate": {"value": v_n * S / len(cpus),
+                            "how": f"measured {len(cpus)}-core rate x {S}/{len(cpus)} (the per-thread flavour has no "
+                                   f"shared state; the job's CPU share is {len(cpus)} cores, not the socket)"},
+        "as_written": {"value": v_a, "kind": "reference",
+                       "sample": f"oracle/_ref/rt (src/rt.cpp unchanged: one erand48 state shared by all threads, "
+                                 f"SURVEY H4), `rt {spp_a}`, {len(cpus)} threads on the same cores, {el_a:.2f}s"},
+    }
+    res.update(reference_rows_check(img, c))
+    return res
 
 
 def pmc_profile(config: str, world: int):
@@ -149,49 +248,25 @@ def pmc_fp64_flop(prof):
         return None
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="ff", choices=list(CONFIGS))
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--chunk", type=int, default=0, help="samples per work unit (0 = auto: 32, more above 4096 spp, tapered; vpt_chunks.h)")
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="steps in flight: each on its own context + HIP stream, so one launch's drain (its "
-                         "last, longest paths) overlaps the next launch's start; 1 = strictly serialized")
-    args = ap.parse_args()
+def measure(c: dict, args, tracers, streams, world: int, rank: int, dev) -> dict:
+    """Times args.steps images of config `c` (after args.warmup untimed ones), every rank
+    rendering its row bands, strips gathered to rank 0 (N > 1); max over ranks.  Returns the
+    whole-job rate, the kernel's serialized launch time (HIP events on the launch stream) and the
+    ray-sphere tests per sample of the reference algorithm on this workload."""
+    import torch.distributed as tdist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
-
-    c = CONFIGS[args.config]
+    dist = tdist if world > 1 else None
     H, W, SPP = c["height"], c["width"], c["spp"]
     band = BAND_ROWS if world > 1 else H
     if world > 1 and H % (band * world):
         raise SystemExit("image height must be a multiple of 16 * world size")
     cfg = vpt.RenderConfig(**c, seed=0x5EED0001, band_rows=band, band_stride=world, band_offset=rank,
                            chunk_spp=args.chunk)
-    D = max(1, args.inflight)
-    tracers = [vpt.Tracer(dev.index) for _ in range(D)]  # one context (work queue, partials) per slot
-    tracer = tracers[0]
+    D = len(tracers)
+    tracer, stream = tracers[0], streams[0]
     rows = cfg.shard_rows()
     outs = [torch.empty((rows, W, 3), dtype=torch.float32, device=dev) for _ in range(D)]
     images = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) if rank == 0 else None for _ in range(D)]
-    streams = [torch.cuda.current_stream(dev)] if D == 1 else [torch.cuda.Stream(dev) for _ in range(D)]
-    stream = streams[0]
 
     # ray-sphere tests per sample of the reference algorithm on this workload (counting build of
     # the same kernel, untimed; 1/16 of the spp -- the per-sample mean is what is needed)
@@ -249,66 +324,147 @@ def main() -> None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    samples_step = H * W * SPP
-    value = samples_step * args.steps / elapsed / 1e6
-    launch_samples = rows * W * SPP
-    achieved = launch_samples * FLOP_PER_TEST * T / (kern_ms * 1e-3) / 1e12
-    prof = pmc_profile(args.config, world)
-    full = pmc_fp64_flop(prof)
+    img = None
     if rank == 0:
         for j in range(1, min(D, args.steps)):  # every slot rendered the same image
             assert torch.equal(images[j], images[0]), "in-flight slots disagree"
         img = images[0].float().cpu().numpy()
+    launch_samples = rows * W * SPP
+    achieved = launch_samples * FLOP_PER_TEST * T / (kern_ms * 1e-3) / 1e12
+    return {"value": H * W * SPP * args.steps / elapsed / 1e6, "elapsed": elapsed, "kern_ms": kern_ms, "T": T,
+            "achieved": achieved, "launch_samples": launch_samples, "image": img, "band": band, "D": D,
+            "nevents": len(evs)}
+
+
+def workload_name(c: dict) -> str:
+    return (f"{c['estimator']} {c['width']}x{c['height']}x{c['spp']}spp default scene, sigma_a {c['sigma_a']} "
+            f"sigma_s {c['sigma_s']}" + (f", HG g {c['hg_g']}" if c.get("hg_g") else "")
+            + (f", max depth {c['max_depth']}" if c.get("max_depth") else ""))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="ff", choices=list(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the second measurement of BASELINE.json configs[2] (the north-star workload)")
+    ap.add_argument("--chunk", type=int, default=0, help="samples per work unit (0 = auto: 32, more above 4096 spp, tapered; vpt_chunks.h)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="steps in flight: each on its own context + HIP stream, so one launch's drain (its "
+                         "last, longest paths) overlaps the next launch's start; 1 = strictly serialized")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    c = CONFIGS[args.config]
+    D = max(1, args.inflight)
+    tracers = [vpt.Tracer(dev.index) for _ in range(D)]  # one context per slot (each its own stream state)
+    streams = [torch.cuda.current_stream(dev)] if D == 1 else [torch.cuda.Stream(dev) for _ in range(D)]
+    m = measure(c, args, tracers, streams, world, rank, dev)
+    ns = None
+    if args.config == "ff" and not args.no_north_star:
+        ns = measure(CONFIGS[NORTH_STAR], args, tracers, streams, world, rank, dev)
+    prof = pmc_profile(args.config, world)
+    full = pmc_fp64_flop(prof)
+    kern_ms, T = m["kern_ms"], m["T"]
+    if rank == 0:
+        img = m["image"]
+        H, W, SPP = c["height"], c["width"], c["spp"]
         res = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": round(m["value"], 3),
             "unit": "Msamples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(m["elapsed"] / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: the reference's default scene/camera/medium, per-sample erand48 streams (seed 0x5EED0001)",
             "config": {
-                "workload": f"{c['estimator']} {W}x{H}x{SPP}spp default scene, sigma_a {c['sigma_a']} sigma_s {c['sigma_s']}"
-                            + (f", HG g {c['hg_g']}" if c.get("hg_g") else "") + (f", max depth {c['max_depth']}" if c.get("max_depth") else ""),
+                "workload": workload_name(c),
                 "width": W, "height": H, "spp": SPP, "estimator": c["estimator"],
-                "parallelism": f"row bands of {band} interleaved over {world} GPU(s), RCCL gather to rank 0" if world > 1
-                else "1 GPU",
+                "parallelism": f"row bands of {m['band']} interleaved over {world} GPU(s), RCCL gather to rank 0"
+                if world > 1 else "1 GPU",
                 "inflight": D,
             },
             "roofline": {
-                "bound": "mfma",
-                "achieved": round(achieved, 4),
+                "bound": "fp64_valu",
+                "achieved": round(m["achieved"], 4),
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
+                "frac": round(m["achieved"] / FP64_PEAK_TFLOPS, 5),
+                "peak_no_fma": FP64_PEAK_TFLOPS / 2,
+                "frac_of_no_fma_peak": round(m["achieved"] / (FP64_PEAK_TFLOPS / 2), 5),
                 "traffic": pmc_traffic(prof),
                 "kernel": f"pool_kernel<{'FF' if c['estimator'] == 'ff' else 'MIS'}> + reduce_kernel (one launch pair)",
                 "kernel_ms": round(kern_ms, 3),
                 "kernel_ms_from": "HIP events around each launch of the timed steps on their stream" if D == 1 else
-                                  f"HIP events around {len(evs)} serialized launches of the same render on one stream, "
+                                  f"HIP events around {m['nevents']} serialized launches of the same render on one stream, "
                                   f"right after the timed region (its {D} in-flight steps overlap)",
                 "algorithmic": f"{FLOP_PER_TEST} FP64 flop x {T:.2f} ray-sphere tests per sample (SURVEY 8d) x "
-                               f"{launch_samples} samples per launch",
+                               f"{m['launch_samples']} samples per launch",
                 "all_fp64_tflops": round(full / (kern_ms * 1e-3) / 1e12, 3) if full else None,
                 "all_fp64_frac": round(full / (kern_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4) if full else None,
-                "note": "FP64 compute roof: MI355X FP64 vector and FP64 matrix peaks are both 78.6 TFLOP/s (spec); "
-                        "the kernel runs on the FP64 VALU, no MFMA (no dense contraction exists). achieved/frac "
-                        "count intersection flops only (SURVEY 8d); all_fp64_* count every FP64 VALU op of the "
-                        "kernel (committed PMC profile of this command, profiles/r*/pmc_pool_kernel.json)",
+                "note": "FP64 VALU bound (no dense contraction exists, no MFMA): peak 78.6 TFLOP/s counts an FMA as "
+                        "2 flop; the path runs with contraction off (the reference's rounding), so 39.3 TFLOP/s "
+                        "(peak_no_fma) is the ceiling for its separately rounded mul/add. achieved/frac count "
+                        "intersection flops only (SURVEY 8d); all_fp64_* count every FP64 VALU op of the kernel "
+                        "(committed PMC profile of this command, profiles/r*/pmc_pool_kernel.json)",
             },
             "image_mean": [round(float(x), 6) for x in img.reshape(-1, 3).mean(0)],
         }
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         if world == 1 and not args.no_cpu:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            res["cpu_baseline"] = cpu_baseline(threads)
-            # the per-thread-RNG flavour + the per-channel RMSE of sampled rows vs the GPU image
-            res["cpu_baseline"]["port_per_sample_rng"] = cpu_port_check(img, c, threads)
+            res["cpu_baseline"] = cpu_baseline(img, c, threads)
+            res["cpu_baseline"]["port_per_sample_rng"] = cpu_port_check(img, c, threads, bands=4)
+        if ns is not None:
+            cn = CONFIGS[NORTH_STAR]
+            o = {"workload": workload_name(cn) + " (BASELINE.json configs[2])",
+                 "value": round(ns["value"], 3), "unit": "Msamples/s",
+                 "ms_per_step": round(ns["elapsed"] / args.steps * 1e3, 3),
+                 "kernel_ms": round(ns["kern_ms"], 3),
+                 "tests_per_sample": round(ns["T"], 3),
+                 "roofline_frac": round(ns["achieved"] / FP64_PEAK_TFLOPS, 5),
+                 "image_mean": [round(float(x), 6) for x in ns["image"].reshape(-1, 3).mean(0)]}
+            cb = res.get("cpu_baseline")
+            if cb:
+                # the reference's own MIS estimator (MISVPTTracerRecursive, isotropic phase: HG is an
+                # extension), one core, on rows of this image; scaled to the socket by the measured
+                # per-thread-flavour parallel efficiency
+                from oracle.oracle import Reference  # cpu_baseline leg only
+
+                ref = Reference()
+                ref.set_scene(ref.default_scene())
+                t = time.time()
+                ref.render(cn["width"], cn["height"], 32, 1, cn["sigma_a"], cn["sigma_s"], seed=0x5EED0001, y0=512, y1=514)
+                mis1 = 2 * cn["width"] * 32 / (time.time() - t) / 1e6
+                sock = mis1 * cb["parallel_efficiency"] * cb["socket_physical_cores"]
+                o["cpu_reference"] = {"one_core": mis1, "socket_estimate": sock,
+                                      "how": "reference MISVPTTracerRecursive (oracle/_ref/libvpt_ref.so), 2 rows x "
+                                             f"{cn['width']} x 32 spp on one core, x parallel efficiency "
+                                             f"{cb['parallel_efficiency']:.2f} x {cb['socket_physical_cores']} cores"}
+                o["speedup_vs_cpu_socket"] = round(ns["value"] / sock, 1)
+                o["target_speedup"] = 100
+            res["north_star"] = o
         print(json.dumps(res))
     for t in tracers:
         t.close()
