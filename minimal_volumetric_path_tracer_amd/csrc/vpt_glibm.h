@@ -137,6 +137,97 @@ VM_QUAL double gm_sc(vm_ct* K, double x, int cosine)
 VM_QUAL double gm_sin(double x) { return gm_sc(vm_tab(gm_sc_tab), x, 0); }
 VM_QUAL double gm_cos(double x) { return gm_sc(vm_tab(gm_sc_tab), x, 1); }
 
+/* sin(x) and cos(x) together: exactly gm_sc(K, x, 0) and gm_sc(K, x, 1), with the work they share
+ * done once.  For every argument range glibc's __sin and __cos call, between them, ONE do_sin (or
+ * TAYLOR_SIN) and ONE do_cos:
+ *     |x| < 0.855469        sin = do_sin(x, 0)          cos = do_cos(x, 0)
+ *     |x| < 2.426265        sin = +-do_cos(h, hp1)      cos = do_sin(hs, (h - hs) + hp1)
+ *     otherwise, n = x 2/pi sin and cos = +-do_sin(b, db) and +-do_cos(b, db), by the parity of n
+ * (h = hp0 - |x|, hs = h + hp1; b + db = x - n pi/2, reduced once).  So the reduction runs once,
+ * one do_sin/Taylor and one do_cos are evaluated (gm_sc evaluates all three forms per call), and
+ * in the first and last ranges both read the same __sincostab entries (k = round(128 |a|)); in the
+ * middle range the two indices differ only when 128 |h| is within an ulp of a half-integer.  Both
+ * entry sets are read unconditionally (same cache lines; re-reading them only when some lane of
+ * the wave needed it, behind a ballot, was 21 % slower on the pool kernel: A/B 58.6 vs 70.9 ms).
+ * FF 1024^2 x 256: 61.9 ms with two gm_sc calls -> 58.6 ms. */
+VM_QUAL void gm_sincos_fused(vm_ct* K, double x, double* sn_out, double* cs_out)
+{
+    const uint32_t kx = (uint32_t)gm_hi(x) & 0x7fffffffu;
+    const double ax = vm_fabs(x);
+    /* reduce_sincos, as in gm_sc */
+    const double t = gm_fma(x, VM_T(K, GS_HPINV), VM_T(K, GS_TOINT));
+    const double xn = t - VM_T(K, GS_TOINT);
+    const int n0 = (int)(gm_lo(t) & 3u);
+    const double y = gm_fnma(xn, VM_T(K, GS_MP2), gm_fnma(xn, VM_T(K, GS_MP1), x));
+    const double t2 = gm_fnma(xn, VM_T(K, GS_PP3), y);
+    double db = gm_fnma(VM_T(K, GS_PP3), xn, y - t2);
+    const double b = gm_fnma(xn, VM_T(K, GS_PP4), t2);
+    db = db + gm_fnma(xn, VM_T(K, GS_PP4), t2 - b);
+    const double hp1 = VM_T(K, GS_HP1);
+    const double h = VM_T(K, GS_HP0) - ax;
+    const double hs = h + hp1;
+    const int r2 = kx < 0x3feb6000u, r3 = kx < 0x400368fdu;
+    /* operands of the do_sin/Taylor evaluation (S) and of the do_cos evaluation (C) */
+    const double aS = r2 ? x : r3 ? hs : b;
+    const double daS = r2 ? 0.0 : r3 ? (h - hs) + hp1 : db;
+    const double aC = r2 ? x : r3 ? h : b;
+    const double daC = r2 ? 0.0 : r3 ? hp1 : db;
+    /* S: do_sin(aS, daS), or TAYLOR_SIN for |aS| < 0.126 */
+    const double aaS = vm_fabs(aS);
+    const double dxS = aS < 0 ? -daS : daS;
+    const double uS = aaS + VM_T(K, GS_BIG);
+    uint32_t kS = gm_lo(uS) << 2;
+    kS = kS < 436u ? kS : 436u;
+    const double xS = aaS - (uS - VM_T(K, GS_BIG));
+    /* C: do_cos(aC, daC) */
+    const double aaC = vm_fabs(aC);
+    const double dxC = aC < 0 ? -daC : daC;
+    const double uC = aaC + VM_T(K, GS_BIG);
+    uint32_t kC = gm_lo(uC) << 2;
+    kC = kC < 436u ? kC : 436u;
+    const double xC = (aaC - (uC - VM_T(K, GS_BIG))) + dxC;
+    const double snS = GM_SINCOSTAB[kS], ssnS = GM_SINCOSTAB[kS + 1];
+    const double csS = GM_SINCOSTAB[kS + 2], ccsS = GM_SINCOSTAB[kS + 3];
+    const double snC = GM_SINCOSTAB[kC], ssnC = GM_SINCOSTAB[kC + 1];
+    const double csC = GM_SINCOSTAB[kC + 2], ccsC = GM_SINCOSTAB[kC + 3];
+    /* do_sin: s = x + (dx + x xx P), c = x dx + xx C, copysign(sn + cor, a) */
+    const double xxS = xS * xS;
+    const double psS = gm_fma(VM_T(K, GS_SN5), xxS, VM_T(K, GS_SN3));
+    double pcS = gm_fma(VM_T(K, GS_CS6), xxS, VM_T(K, GS_CS4));
+    pcS = gm_fma(pcS, xxS, 0.5);
+    const double s_s = xS + gm_fma(xS * xxS, psS, dxS);
+    const double c_s = gm_fma(xS, dxS, xxS * pcS);
+    const double vS = vm_copysign(snS + gm_fma(s_s, csS, gm_fnma(c_s, snS, gm_fma(s_s, ccsS, ssnS))), aS);
+    /* TAYLOR_SIN(aS^2, aS, daS) */
+    const double xx0 = aS * aS;
+    double p = gm_fma(VM_T(K, GS_S5), xx0, VM_T(K, GS_S5 + 1));
+    p = gm_fma(p, xx0, VM_T(K, GS_S5 + 2));
+    p = gm_fma(p, xx0, VM_T(K, GS_S5 + 3));
+    p = gm_fma(p, xx0, VM_T(K, GS_S5 + 4));
+    const double vT = gm_fma(xx0, fma(p, aS, -(0.5 * daS)), daS) + aS;
+    const double vSin = aaS < VM_T(K, GS_TAYLOR) ? vT : vS;
+    /* do_cos: s = x + x xx P, cs + (((ccs - s ssn) - cs c) - sn s) */
+    const double xxC = xC * xC;
+    const double psC = gm_fma(VM_T(K, GS_SN5), xxC, VM_T(K, GS_SN3));
+    double pcC = gm_fma(VM_T(K, GS_CS6), xxC, VM_T(K, GS_CS4));
+    pcC = gm_fma(pcC, xxC, 0.5);
+    const double s_c = gm_fma(xC * xxC, psC, xC);
+    const double vCos = csC + gm_fnma(s_c, snC, gm_fnma(xxC * pcC, csC, gm_fnma(s_c, ssnC, ccsC)));
+    /* which evaluation is whose, and the signs */
+    const int odd = n0 & 1;
+    double s = (r2 || (!r3 && !odd)) ? vSin : vCos;
+    double c = (r2 || (!r3 && !odd)) ? vCos : vSin;
+    const int sflip = r2 ? 0 : r3 ? (x < 0) : (n0 & 2) != 0;
+    const int cflip = (r2 || r3) ? 0 : ((n0 + 1) & 2) != 0;
+    s = sflip ? -s : s;
+    c = cflip ? -c : c;
+    s = kx < 0x3e500000u ? x : s;
+    c = kx < 0x3e400000u ? 1.0 : c;
+    const double nan = x - x + __builtin_nan("");
+    *sn_out = kx >= 0x419921fbu ? nan : s;
+    *cs_out = kx >= 0x419921fbu ? nan : c;
+}
+
 /* ------------------------------------------------------------------ acos (e_asin.c) */
 /* __ieee754_acos.  For 0.125 <= |x| < 0.96875 glibc splits [0.125, 1) into intervals
  * (32 + 64 of width 2^-8 / 2^-7 below 0.5, then 2^-6 ... ) and evaluates, around each interval's
@@ -155,6 +246,7 @@ enum { GA_F6 = 0, GA_RT3 = 6, GA_T27 = 10, GA_HP0, GA_HP1, GA_PI };
 VM_QUAL double gm_acos(double x)
 {
     vm_ct* K = vm_tab(gm_acos_tab);
+    const double HP0 = VM_T(K, GA_HP0), HP1 = VM_T(K, GA_HP1);
     const int32_t m = gm_hi(x);
     const uint32_t k = (uint32_t)m & 0x7fffffffu;
     const double xa = m > 0 ? x : -x;
@@ -174,9 +266,13 @@ VM_QUAL double gm_acos(double x)
         p = gm_fma(p, xx * xx, T[d + 1]);
         const double t = gm_fma(xx, T[1], p);
         const double y = T[d + 2];
-        res = m > 0 ? (VM_T(K, GA_HP1) - t) + (VM_T(K, GA_HP0) - y) : (t + VM_T(K, GA_HP1)) + (y + VM_T(K, GA_HP0));
-    } else if (k >= 0x3fef0000u && k < 0x3ff00000u) {
-        /* 0.96875 <= |x| < 1: acos = 2 asin(sqrt(z)) or pi - that, z = (1 - |x|)/2 */
+        res = m > 0 ? (HP1 - t) + (HP0 - y) : (t + HP1) + (y + HP0);
+    } else {
+        /* 0.96875 <= |x| < 1 (B): acos = 2 asin(sqrt(z)) or pi - that, z = (1 - |x|)/2;
+         * |x| < 0.125 (C; hp0 for |x| < 2^-55); |x| = 1; |x| > 1 and NaN.  B and C evaluate the same
+         * odd asin polynomial (in z, in x^2): one path, one Horner loop, the result selected (a
+         * wave of the cosine-hemisphere or isotropic samplers usually holds lanes of both) */
+        const int isB = k >= 0x3fef0000u && k < 0x3ff00000u;
         const double z = (m > 0 ? 1.0 - x : x + 1.0) * 0.5;
         const uint64_t zb = vm_as_u64(z);
         const double two = vm_as_f64((uint64_t)(511 - (int)(zb >> 53) + 1023) << 52);  /* powtwo[] */
@@ -190,25 +286,119 @@ VM_QUAL double gm_acos(double x)
         const double t27 = VM_T(K, GA_T27);
         const double y = gm_fnma(t27, c, gm_fma(c, t27, c));
         const double cc = gm_fnma(y, y, z) / gm_fma(h, c, y);
-        double p;
-        VM_HORNER_T(p, K + GA_F6, 6, z);
-        const double pr = (p * z) * (y + cc);
-        const double s = m >= 0 ? (cc + pr) + y : ((VM_T(K, GA_HP1) - cc) - pr) + (VM_T(K, GA_HP0) - y);
-        res = s + s;
-    } else {
-        /* |x| < 0.125 (and hp0 for |x| < 2^-55); |x| = 1; |x| > 1 and NaN */
         const double x2 = x * x;
         double p;
-        VM_HORNER_T(p, K + GA_F6, 6, x2);
-        const double hp0 = VM_T(K, GA_HP0);
-        const double r = hp0 - x;
-        const double c = (((hp0 - r) - x) + VM_T(K, GA_HP1));
-        res = r + gm_fnma(p, x * x2, c);
-        res = k < 0x3c880000u ? hp0 : res;
-        if (k >= 0x3ff00000u)
-            res = k == 0x3ff00000u && gm_lo(x) == 0 ? (m > 0 ? 0.0 : VM_T(K, GA_PI)) : x - x + __builtin_nan("");
+        const double zp = isB ? z : x2;
+        VM_HORNER_T(p, K + GA_F6, 6, zp);
+        const double pr = (p * z) * (y + cc);
+        const double s = m >= 0 ? (cc + pr) + y : ((HP1 - cc) - pr) + (HP0 - y);
+        const double rc = HP0 - x;
+        const double c0 = (((HP0 - rc) - x) + HP1);
+        double resC = rc + gm_fnma(p, x * x2, c0);
+        resC = k < 0x3c880000u ? HP0 : resC;
+        const double pi = VM_T(K, GA_PI);
+        resC = k >= 0x3ff00000u ? (k == 0x3ff00000u && gm_lo(x) == 0 ? (m > 0 ? 0.0 : pi)
+                                                                      : x - x + __builtin_nan(""))
+                                : resC;
+        res = isB ? s + s : resC;
     }
     return res;
+}
+
+/* ------------------------------------------------------------------ exp / log (e_exp.c, e_log.c)
+ * glibc 2.35's exp and log (the table-driven ones of sysdeps/ieee754/dbl-64, N = 128), FMA build.
+ * The common paths are restated here as straight-line code reading the library's own tables (the
+ * image in vpt_glibc.h: gl_tab); the rare arguments -- exp: |x| >= 512 or |x| < 2^-54, NaN, inf;
+ * log: x <= 0, subnormal, inf, NaN -- go to the translated functions gl_exp / gl_log, in a branch
+ * that a wave enters only when one of its lanes has such an argument.  log's two common paths (|x - 1|
+ * < 0x1.09p-4, and the table path) are both evaluated and selected: log(1 - xi) of a uniform draw
+ * takes the first in ~6 % of lanes, i.e. in most waves. */
+VM_TABLE(gm_exp_tab, {
+    0x1.71547652b82fep7, 0x1.8p52, -0x1.62e42fefa0000p-8, -0x1.cf79abc9e3b3ap-47,  /* 0-3 InvLn2N, Shift, NegLn2hiN/loN */
+    0x1.ffffffffffdbdp-2, 0x1.555555555543cp-3, 0x1.55555cf172b91p-5, 0x1.1111167a4d017p-7})  /* 4-7 C2..C5 */
+VM_TABLE(gm_log_tab, {
+    /* 0-10 the |x - 1| < 0x1.09p-4 polynomial (B), in the order the FMA build uses them */
+    -0x1.ffffffffffdcbp-3, 0x1.5555555555577p-2, 0x1.24924a344de3p-3, -0x1.55555556745a7p-3,
+    -0x1.999eb43b068ffp-4, 0x1.c7184282ad6cap-4, 0x1.999999995dd0cp-3, -0x1.fffffa4423d65p-4,
+    0x1.78182f7afd085p-4, -0x1.5521375d145cdp-4, 0x1p27,
+    /* 11-18 the table path: Ln2hi, Ln2lo, A (in use order) */
+    0x1.62e42fefa3800p-1, 0x1.ef35793c76730p-45, -0x1.fffffffeb4590p-3, 0x1.555555551305bp-2,
+    -0x1.55575e506c89fp-3, 0x1.999b324f10111p-3, -0x1.0000000000001p-1})
+enum { GE_INVLN2N = 0, GE_SHIFT, GE_NLN2HI, GE_NLN2LO, GE_C2, GE_C3, GE_C4, GE_C5 };
+enum { GL_B0 = 0, GL_TWO27 = 10, GL_LN2HI, GL_LN2LO, GL_A0, GL_A1, GL_A2, GL_A3, GL_AH };
+
+/* __exp_data.tab (tail, scale bits) and __log_data.tab (invc, logc), 128 pairs each, in gl_tab */
+#define GM_EXP_T(i) gl_tab[(0xAF9D0ull - GL_TAB_LO) / 8 + (i)]
+#define GM_LOG_T(i) gl_tab[(0xB0270ull - GL_TAB_LO) / 8 + (i)]
+
+VM_QUAL double gm_exp(double x)
+{
+    vm_ct* K = vm_tab(gm_exp_tab);
+    const uint32_t abstop = (uint32_t)(vm_as_u64(x) >> 52) & 0x7ffu;
+    const double z = gm_fma(x, VM_T(K, GE_INVLN2N), VM_T(K, GE_SHIFT));
+    const uint64_t ki = vm_as_u64(z);
+    const double kd = z - VM_T(K, GE_SHIFT);
+    double r = gm_fma(kd, VM_T(K, GE_NLN2HI), x);
+    r = gm_fma(kd, VM_T(K, GE_NLN2LO), r);
+    const uint32_t idx = 2u * (uint32_t)(ki & 0x7fu);
+    const double tail = vm_as_f64(GM_EXP_T(idx));
+    const uint64_t sbits = GM_EXP_T(idx + 1) + (ki << 45);
+    const double r2 = r * r;
+    const double p23 = gm_fma(r, VM_T(K, GE_C3), VM_T(K, GE_C2));
+    const double p45 = gm_fma(r, VM_T(K, GE_C5), VM_T(K, GE_C4));
+    const double tmp = gm_fma(r2 * r2, p45, gm_fma(p23, r2, r + tail));
+    const double scale = vm_as_f64(sbits);
+    double v = gm_fma(scale, tmp, scale);
+    if (abstop - 0x3c9u >= 0x3fu) v = gl_exp(x);
+    return v;
+}
+
+VM_QUAL double gm_log(double x)
+{
+    vm_ct* K = vm_tab(gm_log_tab);
+    const uint64_t ix = vm_as_u64(x);
+    const uint32_t top = (uint32_t)(ix >> 48);
+    /* |x - 1| < 0x1.09p-4: log1p-style polynomial with an exact head */
+    const double r1 = x - 1.0;
+    const double rr = r1 * r1;
+    const double r3 = r1 * rr;
+    double a = gm_fma(r1, VM_T(K, GL_B0), VM_T(K, GL_B0 + 1));
+    double b = gm_fma(r1, VM_T(K, GL_B0 + 2), VM_T(K, GL_B0 + 3));
+    double c = gm_fma(r1, VM_T(K, GL_B0 + 4), VM_T(K, GL_B0 + 5));
+    a = gm_fma(rr, VM_T(K, GL_B0 + 6), a);
+    b = gm_fma(rr, VM_T(K, GL_B0 + 7), b);
+    c = gm_fma(rr, VM_T(K, GL_B0 + 8), c);
+    c = gm_fma(r3, VM_T(K, GL_B0 + 9), c);
+    c = gm_fma(c, r3, b);
+    c = gm_fma(c, r3, a);
+    const double two27 = VM_T(K, GL_TWO27);
+    const double rhi = gm_fnma(two27, r1, gm_fma(r1, two27, r1));
+    const double rhi2 = rhi * rhi;
+    const double ah = -0.5;  /* B0 of glibc's table */
+    const double hi1 = gm_fma(rhi2, ah, r1);
+    double lo1 = gm_fma(rhi2, ah, r1 - hi1);
+    lo1 = gm_fma(ah * (r1 - rhi), r1 + rhi, lo1);
+    double v1 = hi1 + gm_fma(c, r3, lo1);
+    v1 = ix == 0x3ff0000000000000ull ? 0.0 : v1;
+    /* table path: x = 2^k z, z near 1/invc, log x = k ln2 + logc + log(z invc) */
+    const uint64_t tmp = ix + 0xc01a000000000000ull;
+    const uint32_t i = (uint32_t)(tmp >> 45) & 0x7fu;
+    const int k = (int)((int64_t)tmp >> 52);
+    const double zz = vm_as_f64(ix - (tmp & 0xfff0000000000000ull));
+    const double kd = (double)k;
+    const double invc = vm_as_f64(GM_LOG_T(2 * i)), logc = vm_as_f64(GM_LOG_T(2 * i + 1));
+    const double r = gm_fma(zz, invc, -1.0);
+    const double w = gm_fma(kd, VM_T(K, GL_LN2HI), logc);
+    const double hi = r + w;
+    const double r2 = r * r;
+    double lo = gm_fma(kd, VM_T(K, GL_LN2LO), (w - hi) + r);
+    lo = gm_fma(r2, VM_T(K, GL_AH), lo);
+    double q = gm_fma(r, VM_T(K, GL_A2), VM_T(K, GL_A3));
+    q = gm_fma(q, r2, gm_fma(r, VM_T(K, GL_A0), VM_T(K, GL_A1)));
+    const double v2 = gm_fma(r * r2, q, lo) + hi;
+    double v = ix + 0xc012000000000000ull <= 0x308ffffffffffull ? v1 : v2;
+    if (top - 0x0010u >= 0x7ff0u - 0x0010u) v = gl_log(x);
+    return v;
 }
 
 /* Out-of-line entry points for the kernel.  The tracer's direction samplers call acos and four
@@ -228,14 +418,25 @@ typedef struct {
     double s0, c0, s1, c1;
 } gm_sc2;
 
+#ifndef VPT_GM_FUSED
+#define VPT_GM_FUSED 1  /* sin and cos of one argument by gm_sincos_fused (0: two gm_sc calls) */
+#endif
+VM_QUAL void gm_sincos_k(vm_ct* K, double x, double* s, double* c)
+{
+#if VPT_GM_FUSED
+    gm_sincos_fused(K, x, s, c);
+#else
+    *s = gm_sc(K, x, 0);
+    *c = gm_sc(K, x, 1);
+#endif
+}
+
 VM_QUAL gm_sc2 gm_sincos2_inl(double x0, double x1)
 {
     vm_ct* K = vm_tab(gm_sc_tab);
     gm_sc2 r;
-    r.s0 = gm_sc(K, x0, 0);
-    r.c0 = gm_sc(K, x0, 1);
-    r.s1 = gm_sc(K, x1, 0);
-    r.c1 = gm_sc(K, x1, 1);
+    gm_sincos_k(K, x0, &r.s0, &r.c0);
+    gm_sincos_k(K, x1, &r.s1, &r.c1);
     return r;
 }
 
@@ -244,15 +445,17 @@ GM_CALLQ gm_sc2 gm_sincos2(double x0, double x1) { return gm_sincos2_inl(x0, x1)
 
 /* sin(acos c), cos(acos c), sin(phi), cos(phi): the five calls of the reference's direction
  * samplers (include/samplingFunctions.h:47-82, include/vptSamplingFunctions.h:34-47) */
-GM_CALLQ gm_sc2 gm_sincos_acos_phi(double c, double phi) { return gm_sincos2_inl(gm_acos(c), phi); }
+GM_CALLQ gm_sc2 gm_sincos_acos_phi(double c, double phi)
+{
+    return gm_sincos2_inl(gm_acos(c), phi);
+}
 
 /* sin(x), cos(x) */
 GM_CALLQ gm_sc2 gm_sincos1(double x)
 {
     vm_ct* K = vm_tab(gm_sc_tab);
     gm_sc2 r;
-    r.s0 = gm_sc(K, x, 0);
-    r.c0 = gm_sc(K, x, 1);
+    gm_sincos_k(K, x, &r.s0, &r.c0);
     r.s1 = r.c1 = 0.0;
     return r;
 }
