@@ -401,6 +401,70 @@ VM_QUAL double gm_log(double x)
     return v;
 }
 
+/* ------------------------------------------------------------------ atan2 (e_atan2.c)
+ * glibc 2.35's __ieee754_atan2, FMA build, for x > 0: atan(|y|/x) (|y| < x) or pi/2 - atan(x/|y|)
+ * (x <= |y|) from u = min/max and its correction du, by an odd polynomial (u < 1/16) or around a
+ * node of the cij table (7 doubles per node), sign of y.  The four forms are evaluated branch-free
+ * and selected.  Everything else -- x <= 0, y = 0, NaN, inf, |y|/x far outside [2^-57, 2^57] (the
+ * exponent-difference shortcuts), operands the library rescales (below 2^-500 or above 2^500) --
+ * goes to the translated gl_atan2.  The equi-angular setup (include/volumetricBasicFunctions.h:
+ * 209-223) calls atan2(-proj, D) and atan2(tMax - proj, D) with D > 0. */
+VM_TABLE(gm_atan2_tab, {
+    0x1.375f08b31cbcep-4, -0x1.7458022b13c25p-4, 0x1.c71c6e5129a3bp-4, -0x1.24924923f7603p-3,
+    0x1.99999999997fdp-3, -0x1.5555555555555p-2,          /* 0-5 d13 .. d3 */
+    0x1.921fb54442d18p+0, 0x1.1a62633145c07p-54,          /* 6-7 hpi, hpi1 */
+    0x1p-500, 0x1p500, 0x1p52})                           /* 8-10 */
+enum { GT_D13 = 0, GT_HPI = 6, GT_HPI1, GT_TM500, GT_T500, GT_TWO52 };
+#define GM_CIJ(i, j) vm_as_f64(gl_tab[(0xBE0E0ull - GL_TAB_LO) / 8 + 7 * (i) + (j)])
+
+VM_QUAL double gm_atan2(double y, double x)
+{
+    vm_ct* K = vm_tab(gm_atan2_tab);
+    const double ax = vm_fabs(x), ay = vm_fabs(y);
+    const int de = (int)((uint32_t)gm_hi(y) & 0x7ff00000u) - (int)((uint32_t)gm_hi(x) & 0x7ff00000u);
+    const int ci = ax > ay;  /* case (i): atan(ay/ax); else (ii): pi/2 - atan(ax/ay) */
+    const double num = ci ? ay : ax, den = ci ? ax : ay;
+    const double u = num / den;
+    const double v5 = den * u;
+    const double v7 = gm_fma(den, u, -v5);
+    const double du = ((num - v5) - v7) / den;
+    /* u < 1/16: odd polynomial in u */
+    const double v = u * u;
+    double p;
+    VM_HORNER_T(p, K + GT_D13, 6, v);
+    const double uv = u * v;
+    const double hpi = VM_T(K, GT_HPI), hpi1 = VM_T(K, GT_HPI1);
+    const double z_i_poly = u + gm_fma(uv, p, du);
+    const double t2 = hpi - u;
+    const double z_ii_poly = ((((hpi - t2) - u) + hpi1) - du) - uv * p + t2;
+    /* u >= 1/16: around the node i = round(256 u) - 16 */
+    int i = (int)(gm_fma(u, 256.0, VM_T(K, GT_TWO52)) - VM_T(K, GT_TWO52)) - 16;
+    i = i < 0 ? 0 : i > 240 ? 240 : i;
+    const double c0 = GM_CIJ(i, 0), c1 = GM_CIJ(i, 1), c2 = GM_CIJ(i, 2), c3 = GM_CIJ(i, 3);
+    const double c4 = GM_CIJ(i, 4), c5 = GM_CIJ(i, 5), c6 = GM_CIJ(i, 6);
+    const double t3 = u - c0;
+    const double w = du + t3;  /* case (i): EADD(t3, du) */
+    const double dw = vm_fabs(t3) > vm_fabs(du) ? (t3 - w) + du : (du - w) + t3;
+    double q = gm_fma(w, c6, c5);
+    q = gm_fma(w, q, c4);
+    q = gm_fma(w, q, c3);
+    const double z_i_tab = gm_fma(w, c2, gm_fma(dw, c2, (w * w) * q)) + c1;
+    const double w2 = t3 + du;  /* case (ii) */
+    double q2 = gm_fma(w2, c6, c5);
+    q2 = gm_fma(w2, q2, c4);
+    q2 = gm_fma(w2, q2, c3);
+    q2 = gm_fma(w2, q2, c2);
+    const double z_ii_tab = (hpi - c1) + gm_fnma(w2, q2, hpi1);
+    const int small = u < 0.0625;
+    const double z = ci ? (small ? z_i_poly : z_i_tab) : (small ? z_ii_poly : z_ii_tab);
+    double r = vm_copysign(z, y);
+    const double tm500 = VM_T(K, GT_TM500), t500 = VM_T(K, GT_T500);
+    const int rare = !(x > 0.0) || !(ay > 0.0) || !(x < __builtin_inf()) || !(ay < __builtin_inf()) ||
+                     de > 0x38fffff || de < -0x38fffff || ax < tm500 || ay < tm500 || ax > t500 || ay > t500;
+    if (rare) r = gl_atan2(y, x);
+    return r;
+}
+
 /* Out-of-line entry points for the kernel.  The tracer's direction samplers call acos and four
  * sin/cos at ~10 sites per stage; inlined, each site carries its own copy (code size, and
  * registers held across the expansion).  On the device these are real calls (VPT_GM_CALL=1),
