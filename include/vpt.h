@@ -148,6 +148,22 @@ int vpt_render_device(vpt_context* ctx, const vpt_params* p, void* d_out, void* 
 /* Same, synchronous, host output buffer. */
 int vpt_render(vpt_context* ctx, const vpt_params* p, void* h_out);
 
+/* ---- several GPUs of one process ----
+ * One image rendered by devices 0 .. n_gpus-1 of this process (replaces the OpenMP pixel loop of
+ * src/rt.cpp:767-805 on a multi-GPU node without a launcher).  Device g renders the file-row
+ * bands g, g + n_gpus, ... (band_rows of `p` when it cuts the image, else 16 rows; p itself must
+ * describe the whole image: band_stride 1, band_offset 0); the strips are gathered to device 0
+ * over RCCL (one communicator per device, ncclCommInitAll; grouped ncclSend/ncclRecv) and
+ * written to h_out in file order.  Bit-identical to vpt_render for any n_gpus.  Synchronous.
+ * vpt_multi_* keep the contexts, streams, communicators and buffers between images. */
+typedef struct vpt_multi vpt_multi;
+int vpt_multi_create(int n_gpus, vpt_multi** out);
+int vpt_multi_set_scene(vpt_multi* m, const vpt_sphere* spheres, int n);
+int vpt_multi_render(vpt_multi* m, const vpt_params* p, void* h_out);
+void vpt_multi_destroy(vpt_multi* m);
+/* one-shot: create, set the scene, render, destroy */
+int vpt_render_multi(const vpt_sphere* spheres, int n, const vpt_params* p, int n_gpus, void* h_out);
+
 /* The per-sample call itself, batched: rays[i] with erand48 start state states[i] (low 48
  * bits) through the estimator of `m`; out_rgb[3i..3i+2] = the Color the reference returns,
  * out_states[i] (optional) = the erand48 state afterwards.  Host pointers; synchronous. */

@@ -4,12 +4,14 @@ for gfx950 behind a C ABI (include/vpt.h, libvpt.so).  See DESIGN.md."""
 from ._lib import (EXPLICIT_EQUIANGULAR, EXPLICIT_FREE, FB_F32, FB_F64, FREE_FLIGHT, IMPLICIT_FREE, MIS_EQUIANGULAR,
                    RAY_DTYPE, RAY_MARCHING, SPHERE_DTYPE, SURFACE_PT, VPTError, lib)
 from .tracer import (
+    MultiTracer,
     Ray,
     RenderConfig,
     Sphere,
     Tracer,
     default_scene,
     encode_ppm,
+    render_multi,
     scene,
     stream_state,
     write_ppm,
@@ -17,5 +19,5 @@ from .tracer import (
 
 __all__ = [
     "FB_F32", "FB_F64", "FREE_FLIGHT", "MIS_EQUIANGULAR", "EXPLICIT_FREE", "IMPLICIT_FREE", "EXPLICIT_EQUIANGULAR", "SURFACE_PT", "RAY_MARCHING", "RAY_DTYPE", "SPHERE_DTYPE", "VPTError", "lib",
-    "Ray", "RenderConfig", "Sphere", "Tracer", "default_scene", "encode_ppm", "scene", "stream_state", "write_ppm",
+    "MultiTracer", "render_multi", "Ray", "RenderConfig", "Sphere", "Tracer", "default_scene", "encode_ppm", "scene", "stream_state", "write_ppm",
 ]

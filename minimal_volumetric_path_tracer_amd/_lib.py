@@ -87,6 +87,11 @@ PROTOTYPES = [
     ("vpt_set_scene", c_int, [c_void_p, c_void_p, c_int]),
     ("vpt_render_device", c_int, [c_void_p, POINTER(vpt_params), c_void_p, c_void_p]),
     ("vpt_render", c_int, [c_void_p, POINTER(vpt_params), c_void_p]),
+    ("vpt_multi_create", c_int, [c_int, POINTER(c_void_p)]),
+    ("vpt_multi_set_scene", c_int, [c_void_p, c_void_p, c_int]),
+    ("vpt_multi_render", c_int, [c_void_p, POINTER(vpt_params), c_void_p]),
+    ("vpt_multi_destroy", None, [c_void_p]),
+    ("vpt_render_multi", c_int, [c_void_p, c_int, POINTER(vpt_params), c_int, c_void_p]),
     ("vpt_trace_batch", c_int, [c_void_p, POINTER(vpt_medium), c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     ("vpt_count_work", c_int, [c_void_p, POINTER(vpt_params), POINTER(c_uint64), POINTER(c_uint64)]),
     ("vpt_stream_state", c_uint64, [c_uint64, c_uint64, c_uint64]),

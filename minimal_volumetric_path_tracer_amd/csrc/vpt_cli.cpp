@@ -2,11 +2,14 @@
  * vpt_cli.cpp -- the `vpt` program: drop-in for the reference's `./rt <spp>` (src/rt.cpp:744-830).
  *
  *   vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt|ray-marching] [--march-step S] [--march-light I] [--sigma-a A] [--sigma-s S]
- *             [--g G] [--max-depth D] [--seed N] [--device I] [--fp64] [--out image.ppm]
+ *             [--g G] [--max-depth D] [--seed N] [--device I] [--gpus N] [--fp64] [--out image.ppm]
  *
  * With only <spp> it renders the reference's default scene (include/Sphere.cpp:11-22), camera and
  * medium (src/rt.cpp:752-759,794) at 1024x768 with the free-flight estimator, writes image.ppm
  * in the reference's exact format and prints "elapsed time: <s>s" like src/rt.cpp:824-827.
+ * --gpus N renders the image on devices 0 .. N-1 of this process (vpt_render_multi: interleaved
+ * row bands, strips gathered over RCCL) -- the reference's OpenMP loop over all cores, at node
+ * scale; the bytes are the same for any N.
  * Unlike the reference, a missing or bad argument is an error, not undefined behaviour.
  */
 #include <chrono>
@@ -23,7 +26,7 @@ static int usage()
 {
     std::fprintf(stderr,
                  "usage: vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt|ray-marching] [--march-step S] [--march-light I] [--sigma-a A] [--sigma-s S]\n"
-                 "           [--g G] [--max-depth D] [--seed N] [--device I] [--fp64] [--out image.ppm]\n");
+                 "           [--g G] [--max-depth D] [--seed N] [--device I] [--gpus N] [--fp64] [--out image.ppm]\n");
     return 2;
 }
 
@@ -38,7 +41,7 @@ int main(int argc, char** argv)
     if (!end || *end || spp <= 0) return usage();
     p.spp = (int)spp;
     std::string out = "image.ppm";
-    int device = 0;
+    int device = 0, gpus = 0;
     for (int i = 2; i < argc; ++i) {
         std::string a = argv[i];
         auto need = [&](void) -> const char* {
@@ -68,6 +71,10 @@ int main(int argc, char** argv)
         else if (a == "--max-depth") p.medium.max_depth = std::atoi(need());
         else if (a == "--seed") p.seed = std::strtoull(need(), nullptr, 0);
         else if (a == "--device") device = std::atoi(need());
+        else if (a == "--gpus") {
+            gpus = std::atoi(need());
+            if (gpus < 1) return usage();
+        }
         else if (a == "--fp64") p.fb_format = VPT_FB_F64;
         else if (a == "--out") out = need();
         else return usage();
@@ -76,11 +83,16 @@ int main(int argc, char** argv)
     std::vector<vpt_sphere> scene(VPT_MAX_SPHERES);
     int n = vpt_default_scene(scene.data(), (int)scene.size());
     vpt_context* ctx = nullptr;
-    int rc = vpt_context_create(device, &ctx);
-    if (rc == VPT_OK) rc = vpt_set_scene(ctx, scene.data(), n);
     size_t elem = p.fb_format == VPT_FB_F64 ? sizeof(double) : sizeof(float);
     std::vector<char> fb((size_t)p.width * p.height * 3 * elem);
-    if (rc == VPT_OK) rc = vpt_render(ctx, &p, fb.data());
+    int rc = VPT_OK;
+    if (gpus > 0) {
+        rc = vpt_render_multi(scene.data(), n, &p, gpus, fb.data());
+    } else {
+        rc = vpt_context_create(device, &ctx);
+        if (rc == VPT_OK) rc = vpt_set_scene(ctx, scene.data(), n);
+        if (rc == VPT_OK) rc = vpt_render(ctx, &p, fb.data());
+    }
     if (rc == VPT_OK) rc = vpt_write_ppm(out.c_str(), fb.data(), p.fb_format, p.width, p.height);
     if (rc != VPT_OK) {
         std::fprintf(stderr, "vpt: error %d: %s\n", rc, vpt_last_error());

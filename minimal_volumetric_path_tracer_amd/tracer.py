@@ -204,6 +204,51 @@ class Tracer:
         return out
 
 
+class MultiTracer:
+    """Devices 0 .. n_gpus-1 of THIS process rendering one image together (vpt_multi_*, include/vpt.h):
+    interleaved row bands per device, strips gathered to device 0 over RCCL.  Bit-identical to
+    Tracer.render for any n_gpus."""
+
+    def __init__(self, n_gpus: int, spheres: Optional[np.ndarray] = None):
+        h = c_void_p()
+        check(lib().vpt_multi_create(n_gpus, byref(h)))
+        self._m = h
+        self.n_gpus = n_gpus
+        s = np.ascontiguousarray(default_scene() if spheres is None else spheres, dtype=SPHERE_DTYPE)
+        check(lib().vpt_multi_set_scene(self._m, s.ctypes.data, len(s)))
+        self.spheres = s
+
+    def render(self, cfg: Optional[RenderConfig] = None, **kw) -> np.ndarray:
+        """(height, width, 3), file order; cfg.band_rows (when it cuts the image) is the band size."""
+        cfg = cfg or RenderConfig(**kw)
+        p = cfg.params()
+        out = np.zeros((cfg.height, cfg.width, 3), dtype=np.float64 if cfg.fp64 else np.float32)
+        check(lib().vpt_multi_render(self._m, byref(p), out.ctypes.data))
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "_m", None):
+            lib().vpt_multi_destroy(self._m)
+            self._m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render_multi(n_gpus: int, cfg: Optional[RenderConfig] = None, spheres: Optional[np.ndarray] = None,
+                 **kw) -> np.ndarray:
+    """One-shot vpt_render_multi: the image of `cfg` on devices 0 .. n_gpus-1."""
+    cfg = cfg or RenderConfig(**kw)
+    s = np.ascontiguousarray(default_scene() if spheres is None else spheres, dtype=SPHERE_DTYPE)
+    p = cfg.params()
+    out = np.zeros((cfg.height, cfg.width, 3), dtype=np.float64 if cfg.fp64 else np.float32)
+    check(lib().vpt_render_multi(s.ctypes.data, len(s), byref(p), n_gpus, out.ctypes.data))
+    return out
+
+
 # ---- output (src/rt.cpp:812-820) ----
 def _fb(rgb: np.ndarray) -> tuple[np.ndarray, int, int, int]:
     a = np.ascontiguousarray(rgb)
