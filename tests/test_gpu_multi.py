@@ -24,6 +24,7 @@ VPT = os.path.join(ROOT, "minimal_volumetric_path_tracer_amd", "vpt")
 
 @pytest.mark.parametrize("est,fp64", [("ff", True), ("mis", True), ("ff", False)])
 def test_multi_one_gpu_equals_render(gpu_tracer, est, fp64):
+    gpu_tracer.set_scene(vpt.default_scene())
     cfg = vpt.RenderConfig(width=48, height=40, spp=3, estimator=est, fp64=fp64, seed=31)
     ref = gpu_tracer.render(cfg)
     m = vpt.MultiTracer(1)
@@ -38,6 +39,7 @@ def test_multi_one_gpu_equals_render(gpu_tracer, est, fp64):
 
 def test_multi_band_rows_argument(gpu_tracer):
     """a caller band size that cuts the image is accepted (the layout does not change the bits)"""
+    gpu_tracer.set_scene(vpt.default_scene())
     cfg = vpt.RenderConfig(width=32, height=36, spp=2, fp64=True, seed=5)
     ref = gpu_tracer.render(cfg)
     import dataclasses

@@ -530,3 +530,22 @@ def test_large_spp_auto_chunk(gpu_tracer, orc_vm):
     g = gpu_tracer.render(width=8, height=6, spp=5000, seed=12, fp64=True)
     o = orc_vm.render(8, 6, 5000, 0, seed=12, threads=4)
     assert bitwise_equal(g, o).all()
+
+
+# ---- BASELINE.json configs at their exact sample counts and media (small images) ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,w,h,spp,kw", [
+    # configs[2]: MIS (free flight + equi-angular), HG g = 0.5, the default medium, 1024 spp
+    ("mis_hg_1024", 8, 6, 1024, dict(estimator=1, hg_g=0.5)),
+    # configs[4]: MIS at 8192 spp -- the > 4096-spp chunk layout (128 chunks + taper, vpt_chunks.h)
+    ("mis_8192", 4, 3, 8192, dict(estimator=1)),
+    # configs[3]: dense medium (sigma_t 0.03, BASELINE/DESIGN), depth cap 8, 4096 spp
+    ("dense_4096", 4, 3, 4096, dict(estimator=0, sigma_a=0.003, sigma_s=0.027, max_depth=8)),
+])
+def test_baseline_configs_vs_oracle(gpu_tracer, orc_vm, name, w, h, spp, kw):
+    gpu_tracer.set_scene(vpt.default_scene())
+    orc_vm.set_scene(vpt.default_scene())
+    ref = orc_vm.render(w, h, spp, seed=SEED + 17, threads=8, **kw)
+    g = gpu_tracer.render(width=w, height=h, spp=spp, seed=SEED + 17, fp64=True, **kw)
+    assert bitwise_equal(g, ref).all(), (name, np.abs(g - ref).max())
+    assert np.isfinite(g).all() and g.max() > 0, name  # light reaches the camera (dense: sigma_t 0.03)
