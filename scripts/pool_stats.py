@@ -8,10 +8,15 @@ import minimal_volumetric_path_tracer_amd as vpt
 NSTATS = 24
 RINGS = ["A", "S dif/sph", "S dif/pt", "S metal", "S other", "M sph", "M pt"]
 t = vpt.Tracer(0)
-sizes = [(1024, 1024, 256)]
+est = sys.argv[1] if len(sys.argv) > 1 else "ff"
+g = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
+sizes = [(1024, 1024, 256 if est == "ff" else 128)]
 for w, h, spp in sizes:
+    t.render(width=64, height=64, spp=4, estimator=est, hg_g=g)
+    buf0 = (ctypes.c_ulonglong * NSTATS)()
+    vpt.lib().vpt_debug_pool_stats(buf0)  # (reads and clears, if the build clears)
     t0 = time.time()
-    t.render(width=w, height=h, spp=spp)
+    t.render(width=w, height=h, spp=spp, estimator=est, hg_g=g)
     dt = time.time() - t0
     buf = (ctypes.c_ulonglong * NSTATS)()
     vpt.lib().vpt_debug_pool_stats(buf)
