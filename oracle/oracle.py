@@ -56,6 +56,8 @@ _PRIMS = {
     "equiangular_prob": (_D, [_D, _D, _D, _D]),
     "camera_ray": (_U, [_I, _I, _I, _I, _U, _P]),
     "to_display": (_I, [_D]),
+    "punctual_volumetric": (None, [_I, _P, _D, _D, _D, _P]),
+    "ray_marching_explicit": (_U, [_P, _D, _D, _D, _U, _P, _P, _P]),
 }
 
 

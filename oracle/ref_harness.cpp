@@ -107,7 +107,11 @@ void ref_set_scene(const void* in, int n)
  *   3 implicitVPTracerRecursiveFree  vptShadeMethods.h:938
  *   4 explicitVPTracerRecursive      vptShadeMethods.h:1014
  *   5 iterativePathTracer            shadeMethods.h:104 (surface only: sa, ss unused)
- *   6 rayMarching3                   rayMarchingMethods.h:330 (step, idsource: ref_set_march) */
+ *   6 rayMarching3                   rayMarchingMethods.h:330 (step, idsource: ref_set_march)
+ *   7 rayMarching2                   rayMarchingMethods.h:262 (step, idsource)
+ *   8 rayMarchingGlobal              rayMarchingMethods.h:106 (segmentos = the march step parameter)
+ *   9 rayMarching                    rayMarchingMethods.h:34  (sigma_t = sa + ss, steps = the march step
+ *                                                              parameter; the Color it returns) */
 static double g_march_step = 0.1;  /* src/rt.cpp:791 */
 static int g_march_light = 7;
 static Color run_estimator(int estimator, const Ray& r, double sa, double ss)
@@ -119,6 +123,13 @@ static Color run_estimator(int estimator, const Ray& r, double sa, double ss)
     case 3: return implicitVPTracerRecursiveFree(r, sa, ss);
     case 4: return explicitVPTracerRecursive(r, sa, ss, 0);
     case 5: return iterativePathTracer(r);
+    case 7: return rayMarching2(r, sa, ss, g_march_step, g_march_light);
+    case 8: return rayMarchingGlobal(r, sa, ss, g_march_step);
+    case 9: {
+        Point x_new;
+        int idsource = 0;
+        return rayMarching(r, sa + ss, ss, g_march_step, x_new, idsource);
+    }
     default: return rayMarching3(r, sa, ss, g_march_step, g_march_light);
     }
 }
@@ -304,5 +315,24 @@ uint64_t ref_equiangular_params2(int idsource, double tmax, const double ray[6],
 }
 
 double ref_equiangular_prob(double D, double ta, double tb, double s) { return equiAngularProb(D, ta, tb, s); }
+
+/* punctualVolumetric, rayMarchingMethods.h:12 (draws nothing) */
+void ref_punctual_volumetric(int idsource, const double x[3], double phase, double st, double ss, double out[3])
+{
+    put(punctualVolumetric(idsource, V(x), phase, st, ss), out);
+}
+
+/* rayMarching, rayMarchingMethods.h:34, with its two out-parameters: out[0..2] = Color,
+ * out[3..5] = x_new (x_new_in when the ray hits nothing), *idsource (idsource_in on a miss) */
+uint64_t ref_ray_marching_explicit(const double ray[6], double st, double ss, double steps, uint64_t state,
+                                   const double x_new_in[3], int* idsource, double out[6])
+{
+    set_state(state);
+    Point x_new = V(x_new_in);
+    Color c = rayMarching(Ray(V(ray), V(ray + 3)), st, ss, steps, x_new, *idsource);
+    put(c, out);
+    put(x_new, out + 3);
+    return get_state();
+}
 
 }  // extern "C"

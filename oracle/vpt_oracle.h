@@ -28,9 +28,9 @@ typedef struct {
     double sigma_a, sigma_s;  /* src/rt.cpp:794 */
     double hg_g;              /* extension: 0 = reference isotropic phase */
     int32_t max_depth;        /* extension: 0 = unbounded (reference) */
-    int32_t estimator;        /* include/vpt.h vpt_estimator: 0 iterativeVPTracerFree, 1 MISVPTTracerRecursive, ..., 5 iterativePathTracer, 6 rayMarching3 */
-    double march_step;        /* rayMarching3: step */
-    int32_t march_light;      /* rayMarching3: idsource */
+    int32_t estimator;        /* include/vpt.h vpt_estimator: 0 iterativeVPTracerFree, 1 MISVPTTracerRecursive, ..., 5 iterativePathTracer, 6 rayMarching3, 7 rayMarching2, 8 rayMarchingGlobal, 9 rayMarching */
+    double march_step;        /* rayMarching3 / rayMarching2: step; rayMarchingGlobal: segments; rayMarching: steps */
+    int32_t march_light;      /* rayMarching3 / rayMarching2: idsource */
     int32_t reserved_;
 } orc_medium;
 

@@ -62,6 +62,13 @@ def samples_e6():
 
 
 @pytest.fixture(scope="session")
+def samples_e789():
+    """rayMarching2 / rayMarchingGlobal / rayMarching (estimators 7-9), punctualVolumetric and
+    rayMarching's out-parameters (make_golden.py --ray-marching-789)"""
+    return dict(np.load(os.path.join(GOLDEN, "samples_e789.npz")))
+
+
+@pytest.fixture(scope="session")
 def prims():
     return dict(np.load(os.path.join(GOLDEN, "primitives.npz")))
 

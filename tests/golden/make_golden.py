@@ -11,6 +11,7 @@ pins of the oracle.
 """
 from __future__ import annotations
 
+import ctypes
 import json
 import os
 import subprocess
@@ -309,6 +310,80 @@ def ray_marching():
     print("wrote", os.path.join(HERE, "samples_e6.npz"))
 
 
+# rayMarching2 / rayMarchingGlobal / rayMarching cases: (estimator, scene, light index, step or segments);
+# sigma_a 0.001, sigma_s 0.0125 as src/rt.cpp:791.  rayMarchingGlobal and rayMarching sample the
+# hard-coded sphere 5 (include/rayMarchingMethods.h:64,153): the r = 12 area light of alt_area_light,
+# the metal sphere of the default scene.  ("default", 0): rayMarching2's miss id 0 counts as the light.
+E789_CASES = [(7, "default", 7, 0.5), (7, "default", 0, 1.0), (7, "alt_area_light", 5, 0.5), (7, "mat3", 9, 0.75),
+              (8, "alt_area_light", 0, 6.0), (8, "alt_area_light", 0, 2.5), (8, "default", 0, 4.0),
+              (9, "alt_area_light", 0, 10.0), (9, "alt_area_light", 0, 3.5), (9, "default", 0, 10.0)]
+
+
+def ray_marching_789():
+    """rayMarching2 (:262, estimator 7), rayMarchingGlobal (:106, estimator 8), rayMarching (:34,
+    estimator 9) of include/rayMarchingMethods.h, plus known answers for punctualVolumetric (:12) and
+    rayMarching's out-parameters -> samples_e789.npz.  Own RNG seed."""
+    ref = Reference()
+    rng = np.random.default_rng(20261019)
+    scenes = {**EST_SCENES, **ALT_SCENES}
+    bundle = {}
+    for est, name, light, step in E789_CASES:
+        sc = scenes[name]()
+        ref.set_scene(sc)
+        key = f"e{est}_{name}_l{light}_s{step}"
+        bundle[f"{key}__scene"] = sc.view(np.uint8)
+        bundle[f"{key}__march"] = np.array([est, step, light])
+        n = 96
+        xs, ys, si = rng.integers(0, W, n), rng.integers(0, H, n), rng.integers(0, 1 << 20, n)
+        s0 = np.array([stream_state(SEED, int((H - y - 1) * W + x), int(i)) for x, y, i in zip(xs, ys, si)],
+                      dtype=np.uint64)
+        rays = np.zeros((n, 6))
+        s1 = np.zeros(n, dtype=np.uint64)
+        for k in range(n):
+            s1[k] = ref.prim("camera_ray")(W, H, int(xs[k]), int(ys[k]), int(s0[k]), rays[k].ctypes.data)
+        out, s2 = ref.trace(est, rays, s1, 0.001, 0.0125, march_step=step, march_light=light)
+        bundle.update({f"{key}__ray": rays, f"{key}__state1": s1, f"{key}__L": out, f"{key}__state2": s2})
+        bundle[f"{key}__fb16x16x2"] = ref.render(16, 16, 2, est, 0.001, 0.0125, seed=SEED, march_step=step,
+                                                 march_light=light)
+    # punctualVolumetric(idsource, x, phase, sigma_t, sigma_s): every emitter of three scenes
+    for name in ("default", "mat3", "point_lights"):
+        sc = scenes[name]()
+        ref.set_scene(sc)
+        lights = [i for i in range(len(sc)) if sc[i]["radiance"][0] > 0 or sc[i]["radiance"][1] > 0]
+        m = 64 * len(lights)
+        ids = np.repeat(np.array(lights, dtype=np.int64), 64)
+        xp = np.column_stack([rng.uniform(-48, 48, m), rng.uniform(-40, 40, m), rng.uniform(-80, 100, m)])
+        out = np.zeros((m, 3))
+        for k in range(m):
+            ref.prim("punctual_volumetric")(int(ids[k]), np.ascontiguousarray(xp[k]).ctypes.data, 1 / (4 * np.pi),
+                                            0.0135, 0.0125, out[k].ctypes.data)
+        bundle.update({f"pv_{name}__scene": sc.view(np.uint8), f"pv_{name}__id": ids, f"pv_{name}__x": xp,
+                       f"pv_{name}__out": out})
+    # rayMarching's x_new / idsource out-parameters (camera rays of alt_area_light; misses keep the inputs)
+    sc = scenes["alt_area_light"]()
+    ref.set_scene(sc)
+    n = 64
+    rays = np.zeros((n, 6))
+    s1 = np.zeros(n, dtype=np.uint64)
+    for k in range(n):
+        x, y = int(rng.integers(0, W)), int(rng.integers(0, H))
+        s1[k] = ref.prim("camera_ray")(W, H, x, y, stream_state(SEED, (H - y - 1) * W + x, k), rays[k].ctypes.data)
+    rays[::8, 3:6] = (0.0, 1.0, 0.0)  # some rays straight up: alt_area_light has no ceiling (misses)
+    out = np.zeros((n, 6))
+    ids = np.full(n, -1, dtype=np.int32)
+    s2 = np.zeros(n, dtype=np.uint64)
+    xin = np.array([1.5, -2.5, 3.25])
+    for k in range(n):
+        idk = ctypes.c_int(-1)
+        s2[k] = ref.prim("ray_marching_explicit")(rays[k].ctypes.data, 0.0135, 0.0125, 7.0, int(s1[k]),
+                                                  xin.ctypes.data, ctypes.byref(idk), out[k].ctypes.data)
+        ids[k] = idk.value
+    bundle.update({"rmx__ray": rays, "rmx__state1": s1, "rmx__out": out, "rmx__id": ids, "rmx__state2": s2,
+                   "rmx__xin": xin})
+    np.savez_compressed(os.path.join(HERE, "samples_e789.npz"), **bundle)
+    print("wrote", os.path.join(HERE, "samples_e789.npz"))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["--estimators-234"]:
         estimators_234()
@@ -318,9 +393,12 @@ if __name__ == "__main__":
         surface_pt()
     elif sys.argv[1:] == ["--ray-marching"]:
         ray_marching()
+    elif sys.argv[1:] == ["--ray-marching-789"]:
+        ray_marching_789()
     else:
         main()
         estimators_234()
         alt_scenes()
         surface_pt()
         ray_marching()
+        ray_marching_789()

@@ -295,3 +295,63 @@ def test_ray_marching_vs_reference(samples_e6, orc, case):
     # light 7 of the default scene is a sphere light (r = 2): its shadow rays start at its centre and
     # stop on its own surface, so the reference's marching sees it nowhere
     assert (np.abs(out).sum() > 0) == (case != "default_l7")
+
+
+# ---- rayMarching2 (:262, estimator 7), rayMarchingGlobal (:106, estimator 8), rayMarching (:34,
+# estimator 9) of include/rayMarchingMethods.h: same draws, bit-exact values, per sample and 16x16x2
+def _e789_keys():
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "samples_e789.npz")
+    return sorted(k[:-len("__march")] for k in np.load(path).files if k.endswith("__march"))
+
+
+@pytest.mark.parametrize("case", _e789_keys())
+def test_ray_marching_789_vs_reference(samples_e789, orc, case):
+    orc.set_scene(samples_e789[f"{case}__scene"])
+    est, step, light = samples_e789[f"{case}__march"]
+    est, light = int(est), int(light)
+    k = f"{case}__"
+    L, st = orc.trace(est, samples_e789[k + "ray"], samples_e789[k + "state1"], 0.001, 0.0125, march_step=step,
+                      march_light=light)
+    assert np.array_equal(st, samples_e789[k + "state2"])
+    assert bitwise_equal(L, samples_e789[k + "L"]).all()
+    out = orc.render(16, 16, 2, est, 0.001, 0.0125, seed=SEED, threads=2, chunk=2, march_step=step,
+                     march_light=light)
+    assert bitwise_equal(out, samples_e789[k + "fb16x16x2"]).all()
+    # every case draws (solid-angle samples); the default scene's sphere 5 is the unlit metal sphere,
+    # so rayMarching sees no light there (rayMarchingGlobal still returns the lights the camera sees)
+    assert not np.array_equal(samples_e789[k + "state1"], samples_e789[k + "state2"])
+    assert (np.abs(out).sum() > 0) == (not (est == 9 and "default" in case))
+
+
+@pytest.mark.parametrize("scene", ["default", "mat3", "point_lights"])
+def test_punctual_volumetric_vs_reference(samples_e789, orc, scene):
+    """punctualVolumetric (include/rayMarchingMethods.h:12-31): visibilityVPT + multipleT"""
+    orc.set_scene(samples_e789[f"pv_{scene}__scene"])
+    ids, xs, want = samples_e789[f"pv_{scene}__id"], samples_e789[f"pv_{scene}__x"], samples_e789[f"pv_{scene}__out"]
+    got = np.zeros_like(want)
+    f = orc.prim("punctual_volumetric")
+    for k in range(len(ids)):
+        f(int(ids[k]), np.ascontiguousarray(xs[k]).ctypes.data, 1 / (4 * np.pi), 0.0135, 0.0125, got[k].ctypes.data)
+    assert bitwise_equal(got, want).all()
+    assert (want != 0).any() and (want == 0).all(axis=1).any()  # lit and shadowed points both present
+
+
+def test_ray_marching_out_parameters_vs_reference(samples_e789, orc):
+    """rayMarching's x_new / idsource (include/rayMarchingMethods.h:41-44): set on a hit, kept on a miss"""
+    import ctypes
+    from scenes import ALT_SCENES
+    orc.set_scene(ALT_SCENES["alt_area_light"]())
+    rays, s1, xin = samples_e789["rmx__ray"], samples_e789["rmx__state1"], samples_e789["rmx__xin"]
+    out = np.zeros((len(rays), 6))
+    ids = np.zeros(len(rays), dtype=np.int32)
+    s2 = np.zeros(len(rays), dtype=np.uint64)
+    f = orc.prim("ray_marching_explicit")
+    for k in range(len(rays)):
+        idk = ctypes.c_int(-1)
+        s2[k] = f(np.ascontiguousarray(rays[k]).ctypes.data, 0.0135, 0.0125, 7.0, int(s1[k]), xin.ctypes.data,
+                  ctypes.byref(idk), out[k].ctypes.data)
+        ids[k] = idk.value
+    assert bitwise_equal(out, samples_e789["rmx__out"]).all()
+    assert np.array_equal(ids, samples_e789["rmx__id"]) and np.array_equal(s2, samples_e789["rmx__state2"])
+    assert (ids == -1).any() and (ids >= 0).any()
