@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define VPT_ABI_VERSION 2
+#define VPT_ABI_VERSION 3
 
 typedef enum {
     VPT_OK = 0,
@@ -71,12 +71,20 @@ typedef enum {
                                     * commented alternative at src/rt.cpp:793); sigma_a, sigma_s, hg_g and
                                     * max_depth are ignored; renders sum each pixel's samples in the
                                     * reference's sequential order (chunk_spp ignored) */
-    VPT_RAY_MARCHING = 6           /* rayMarching3, rayMarchingMethods.h:330: constant-step marching toward the
+    VPT_RAY_MARCHING = 6,          /* rayMarching3, rayMarchingMethods.h:330: constant-step marching toward the
                                     * light march_light (the commented alternative at src/rt.cpp:791, which
                                     * passes sigma_a 0.001, sigma_s 0.0125, step 0.1, light 7); draws nothing
                                     * beyond the camera jitter; samples summed in the reference's order */
+    VPT_RAY_MARCHING_SA = 7,       /* rayMarching2, rayMarchingMethods.h:262: steps of march_step toward sphere
+                                    * march_light by solid-angle sampling, plus a hit light's radiance */
+    VPT_RAY_MARCHING_GLOBAL = 8,   /* rayMarchingGlobal, rayMarchingMethods.h:106: 10 diffuse bounces, each
+                                    * marched by rayMarching in march_step segments (a count), toward the
+                                    * hard-coded sphere 5 (scenes need >= 6 spheres) */
+    VPT_RAY_MARCHING_EXPLICIT = 9  /* rayMarching, rayMarchingMethods.h:34: the Color it returns for the camera
+                                    * ray with sigma_t = sigma_a + sigma_s, steps = march_step (a count),
+                                    * light = sphere 5; its out-parameters: vpt_ray_marching_batch */
 } vpt_estimator;
-#define VPT_NUM_ESTIMATORS 7
+#define VPT_NUM_ESTIMATORS 10
 
 typedef enum {
     VPT_FB_F32 = 0,            /* framebuffer: 3 x float per pixel */
@@ -90,8 +98,9 @@ typedef struct vpt_medium {
     double hg_g;               /* extension: Henyey-Greenstein g; 0 = the reference's isotropic phase */
     int32_t max_depth;         /* extension: max path vertices; 0 = unbounded (Russian roulette only) */
     int32_t estimator;         /* vpt_estimator */
-    double march_step;         /* VPT_RAY_MARCHING only: step length (> 0; default 0.1) */
-    int32_t march_light;       /* VPT_RAY_MARCHING only: index of the light sphere (default 7) */
+    double march_step;         /* ray marching (6-9): step length (6, 7) or number of segments (8, 9); > 0,
+                                * default 0.1 */
+    int32_t march_light;       /* VPT_RAY_MARCHING, VPT_RAY_MARCHING_SA: index of the light sphere (default 7) */
     int32_t reserved_;
 } vpt_medium;
 
@@ -169,6 +178,20 @@ int vpt_render_multi(const vpt_sphere* spheres, int n, const vpt_params* p, int 
  * out_states[i] (optional) = the erand48 state afterwards.  Host pointers; synchronous. */
 int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, const uint64_t* states, int n,
                     double* out_rgb, uint64_t* out_states);
+
+/* punctualVolumetric(idsource, x, phase, sigma_t, sigma_s) (include/rayMarchingMethods.h:12-31; no
+ * caller in the reference) at the n points x[3i..3i+2]: visibilityVPT from sphere idsource's centre,
+ * radiance / distance^2 * phase * multipleT * sigma_s.  Host arrays; synchronous. */
+int vpt_punctual_volumetric(vpt_context* ctx, int idsource, const double* x, int n, double phase, double sigma_t,
+                            double sigma_s, double* out_rgb);
+
+/* rayMarching(r, sigma_t, sigma_s, steps, x_new, idsource) (include/rayMarchingMethods.h:34-103) for
+ * rays[i] with erand48 start state states[i]: out_rgb = the Color; x_new[3i..] and idsource[i] are
+ * in/out like the reference's reference parameters (set to the first hit, unchanged on a miss);
+ * out_states optional.  Needs >= 6 spheres (sphere 5 is hard-coded).  Host arrays; synchronous. */
+int vpt_ray_marching_batch(vpt_context* ctx, double sigma_t, double sigma_s, double steps, const vpt_ray* rays,
+                           const uint64_t* states, int n, double* out_rgb, double* x_new, int32_t* idsource,
+                           uint64_t* out_states);
 
 /* Counting mode: ray-sphere tests (Sphere::intersect calls, include/Sphere.h:27) the render
  * of `p` performs in the REFERENCE algorithm (shortcuts of this build count what they skip),

@@ -21,6 +21,7 @@ VPT_OK = 0
 VPT_E_INVALID, VPT_E_TOO_MANY, VPT_E_NO_EMITTER, VPT_E_UNSUPPORTED, VPT_E_HIP, VPT_E_IO = -1, -2, -3, -4, -5, -6
 VPT_MAX_SPHERES = 64
 FREE_FLIGHT, MIS_EQUIANGULAR, EXPLICIT_FREE, IMPLICIT_FREE, EXPLICIT_EQUIANGULAR, SURFACE_PT, RAY_MARCHING = 0, 1, 2, 3, 4, 5, 6  # vpt_estimator
+RAY_MARCHING_SA, RAY_MARCHING_GLOBAL, RAY_MARCHING_EXPLICIT = 7, 8, 9
 FB_F32, FB_F64 = 0, 1
 
 # numpy view of vpt_sphere == reference Sphere (include/Sphere.h:12-21), 144 bytes
@@ -93,6 +94,9 @@ PROTOTYPES = [
     ("vpt_multi_destroy", None, [c_void_p]),
     ("vpt_render_multi", c_int, [c_void_p, c_int, POINTER(vpt_params), c_int, c_void_p]),
     ("vpt_trace_batch", c_int, [c_void_p, POINTER(vpt_medium), c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    ("vpt_punctual_volumetric", c_int, [c_void_p, c_int, c_void_p, c_int, c_double, c_double, c_double, c_void_p]),
+    ("vpt_ray_marching_batch", c_int, [c_void_p, c_double, c_double, c_double, c_void_p, c_void_p, c_int, c_void_p,
+                                       c_void_p, c_void_p, c_void_p]),
     ("vpt_count_work", c_int, [c_void_p, POINTER(vpt_params), POINTER(c_uint64), POINTER(c_uint64)]),
     ("vpt_stream_state", c_uint64, [c_uint64, c_uint64, c_uint64]),
     ("vpt_math_probe", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int]),

@@ -1,7 +1,7 @@
 /*
  * vpt_cli.cpp -- the `vpt` program: drop-in for the reference's `./rt <spp>` (src/rt.cpp:744-830).
  *
- *   vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt|ray-marching] [--march-step S] [--march-light I] [--sigma-a A] [--sigma-s S]
+ *   vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt|ray-marching|ray-marching-sa|ray-marching-global|ray-marching-explicit] [--march-step S] [--march-light I] [--sigma-a A] [--sigma-s S]
  *             [--g G] [--max-depth D] [--seed N] [--device I] [--gpus N] [--fp64] [--out image.ppm]
  *
  * With only <spp> it renders the reference's default scene (include/Sphere.cpp:11-22), camera and
@@ -25,7 +25,7 @@
 static int usage()
 {
     std::fprintf(stderr,
-                 "usage: vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt|ray-marching] [--march-step S] [--march-light I] [--sigma-a A] [--sigma-s S]\n"
+                 "usage: vpt <spp> [--width W] [--height H] [--estimator ff|mis|explicit-free|implicit-free|explicit|surface-pt|ray-marching|ray-marching-sa|ray-marching-global|ray-marching-explicit] [--march-step S] [--march-light I] [--sigma-a A] [--sigma-s S]\n"
                  "           [--g G] [--max-depth D] [--seed N] [--device I] [--gpus N] [--fp64] [--out image.ppm]\n");
     return 2;
 }
@@ -62,6 +62,9 @@ int main(int argc, char** argv)
             else if (e == "explicit") p.medium.estimator = VPT_EXPLICIT_EQUIANGULAR;
             else if (e == "surface-pt") p.medium.estimator = VPT_SURFACE_PT;
             else if (e == "ray-marching") p.medium.estimator = VPT_RAY_MARCHING;
+            else if (e == "ray-marching-sa") p.medium.estimator = VPT_RAY_MARCHING_SA;
+            else if (e == "ray-marching-global") p.medium.estimator = VPT_RAY_MARCHING_GLOBAL;
+            else if (e == "ray-marching-explicit") p.medium.estimator = VPT_RAY_MARCHING_EXPLICIT;
             else return usage();
         } else if (a == "--march-step") p.medium.march_step = std::atof(need());
         else if (a == "--march-light") p.medium.march_light = std::atoi(need());

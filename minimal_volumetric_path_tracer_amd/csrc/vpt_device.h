@@ -96,6 +96,46 @@ struct Sampler {
     }
 };
 
+/* One sphere test of Sphere::intersect (include/Sphere.h:27-37) from b = oc.d and det = b^2 - |oc|^2 + r^2:
+ * the reference's
+ *     tact = (t1 < 0 || |t1| < 0.0001) ? t2 : t1,   contact = tact > 0 && |tact| > 0.0001
+ * with t1 = -b - sq, t2 = -b + sq, written with one comparison each: t1 < 0 || |t1| < 0.0001 is
+ * t1 < 0.0001 and tact > 0 && |tact| > 0.0001 is tact > 0.0001, for every t1 / tact including NaN
+ * (ordered comparisons: all false).  tact = 0 (no contact) when det < 0. */
+VPT_DEV double sphere_tact(double b, double det)
+{
+    double tact = 0.0;
+    if (det >= 0) {
+        const double sq = ISECT_SQRT(det);
+        const double t2 = -b + sq;
+        const double t1 = -b - sq;
+        tact = t1 < 0.0001 ? t2 : t1;
+    }
+    return tact;
+}
+
+/* the nearest-contact update of intersect() (include/pathTracingUtilities.h:17-30).  VPT_TAKE_BF=1:
+ * written with selects (A/B: 56.8 -> 57.7 ms at FF 1024^2 x 256, slower) */
+#ifndef VPT_TAKE_BF
+#define VPT_TAKE_BF 0
+#endif
+VPT_DEV void sphere_take(double tact, int i, double& tmin, int& id, int& contact)
+{
+    if (VPT_TAKE_BF) {
+        const bool hit = tact > 0.0001;
+        const bool upd = hit && tact < tmin;
+        contact |= (int)hit;
+        tmin = upd ? tact : tmin;
+        id = upd ? i : id;
+    } else if (tact > 0.0001) {
+        contact = 1;
+        if (tact < tmin) {
+            tmin = tact;
+            id = i;
+        }
+    }
+}
+
 /* ------------------------------------------------------------------ geometry */
 /* Sphere::intersect (include/Sphere.h:27-37) folded into intersect()
  * (include/pathTracingUtilities.h:12-36).  The sphere index is wave-uniform, so the scene
@@ -117,20 +157,7 @@ VPT_DEV int scene_intersect(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
         double b = ocx * d.x + ocy * d.y + ocz * d.z;
         double cc = ocx * ocx + ocy * ocy + ocz * ocz;
         double det = b * b - cc + g.r2;
-        double tact = 0.0;
-        if (det >= 0) {
-            double sq = ISECT_SQRT(det);
-            double t2 = -b + sq;
-            double t1 = -b - sq;
-            tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
-        }
-        if (tact > 0 && vm_fabs(tact) > 0.0001) {
-            contact = 1;
-            if (tact < tmin) {
-                tmin = tact;
-                id = i;
-            }
-        }
+        sphere_take(sphere_tact(b, det), i, tmin, id, contact);
     }
     smp.tests(skip3 ? S->n_non3 : n);
     if (contact) {
@@ -164,25 +191,16 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         }
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            double tact = 0.0;
+            double tact;
             if (VPT_BF_G) {  /* branch-free: the G square-root chains overlap (same values where det >= 0) */
                 const double sq = ISECT_SQRT(det[k] >= 0 ? det[k] : 0.0);
                 const double t2 = -b[k] + sq;
                 const double t1 = -b[k] - sq;
-                tact = det[k] >= 0 ? ((t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1) : 0.0;
-            } else if (det[k] >= 0) {
-                const double sq = ISECT_SQRT(det[k]);
-                const double t2 = -b[k] + sq;
-                const double t1 = -b[k] - sq;
-                tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
+                tact = det[k] >= 0 ? (t1 < 0.0001 ? t2 : t1) : 0.0;
+            } else {
+                tact = sphere_tact(b[k], det[k]);
             }
-            if (tact > 0 && vm_fabs(tact) > 0.0001) {
-                contact = 1;
-                if (tact < tmin) {
-                    tmin = tact;
-                    id = i + k;
-                }
-            }
+            sphere_take(tact, i + k, tmin, id, contact);
         }
     }
     for (; i < n; ++i) {
@@ -191,20 +209,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         const double b = ocx * d.x + ocy * d.y + ocz * d.z;
         const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
         const double det = b * b - cc + g.r2;
-        double tact = 0.0;
-        if (det >= 0) {
-            const double sq = ISECT_SQRT(det);
-            const double t2 = -b + sq;
-            const double t1 = -b - sq;
-            tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
-        }
-        if (tact > 0 && vm_fabs(tact) > 0.0001) {
-            contact = 1;
-            if (tact < tmin) {
-                tmin = tact;
-                id = i;
-            }
-        }
+        sphere_take(sphere_tact(b, det), i, tmin, id, contact);
     }
     smp.tests(n);
     if (contact) {
@@ -659,11 +664,11 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
                                double (&t)[N], int (&id)[N], bool (&hit)[N])
 {
     double tmin[N];
-    bool contact[N];
+    int contact[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         tmin[k] = VPT_DBL_MAX;
-        contact[k] = false;
+        contact[k] = 0;
     }
     const int n = S->n;
     for (int i = 0; i < n; ++i) {
@@ -674,31 +679,22 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
         for (int k = 0; k < N; ++k) {
             const double b = ocx * d[k].x + ocy * d[k].y + ocz * d[k].z;
             const double det = b * b - cc + g.r2;
-            double tact = 0.0;
+            double tact;
             if (VPT_BF_N) {  /* branch-free: the N rays' square-root chains overlap */
                 const double sq = ISECT_SQRT(det >= 0 ? det : 0.0);
                 const double t2 = -b + sq;
                 const double t1 = -b - sq;
-                tact = det >= 0 ? ((t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1) : 0.0;
-            } else if (det >= 0) {
-                const double sq = ISECT_SQRT(det);
-                const double t2 = -b + sq;
-                const double t1 = -b - sq;
-                tact = (t1 < 0 || vm_fabs(t1) < 0.0001) ? t2 : t1;
+                tact = det >= 0 ? (t1 < 0.0001 ? t2 : t1) : 0.0;
+            } else {
+                tact = sphere_tact(b, det);
             }
-            if (tact > 0 && vm_fabs(tact) > 0.0001) {
-                contact[k] = true;
-                if (tact < tmin[k]) {
-                    tmin[k] = tact;
-                    id[k] = i;
-                }
-            }
+            sphere_take(tact, i, tmin[k], id[k], contact[k]);
         }
     }
     smp.tests(N * n);
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        hit[k] = contact[k];
+        hit[k] = contact[k] != 0;
         t[k] = contact[k] ? tmin[k] : 0.0;
     }
 }
@@ -982,7 +978,7 @@ VPT_DEV double equiangular_prob(double D, double ta, double tb, double s) { retu
 struct Medium {
     double sigma_a, sigma_s, g;
     int max_depth;
-    double march_step;  /* rayMarching3 only */
+    double march_step;  /* ray-marching estimators 6-9: step (6, 7) or number of segments (8, 9) */
     int march_light;
 };
 
@@ -1254,6 +1250,146 @@ __device__ static dv3 trace_ray_marching(const DevScene* __restrict__ S, Sampler
     return Li;
 }
 
+/* The step loop of rayMarching (include/rayMarchingMethods.h:55-99), of rayMarchingGlobal's tail
+ * (:208-254) and of rayMarching2 (:280-325): points xt = o + d*step*i for i < n_steps, their
+ * transmittance from x, one solidAngle sample toward sphere `light`, its first hit; the sample
+ * scores when the hit id (0 on a miss: the reference's initialiser) is the light.  Capped like
+ * trace_ray_marching (NaN past VPT_MARCH_MAX_STEPS). */
+template <bool COUNT>
+VPT_DEV dv3 march_solid_angle(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, dv3 x, double n_steps,
+                              double step, int light, double sigma_t, double sigma_s)
+{
+    if (!(n_steps < (double)VPT_MARCH_MAX_STEPS)) return mk(__builtin_nan(""), __builtin_nan(""), __builtin_nan(""));
+    dv3 Li = mk(0, 0, 0);
+    const dv3 lp = sph_p(S, light);
+    const double lr = S->sph[light].r;
+    for (int i = 0; i < n_steps; i++) {
+        if (COUNT) smp.cnt.iterations++;
+        const dv3 xt = add(o, scl(scl(d, step), (double)i));
+        const double T = transmitance(x, xt, sigma_t);
+        const double phase = 1 / (4 * VPT_PI);  /* isotropicPhaseFunction */
+        dv3 wc = sub(lp, xt);
+        const double normcx = vm_sqrt(dot(wc, wc));
+        wc = scl(wc, (1 / normcx));
+        const double cmax = vm_sqrt(1 - (lr / normcx) * (lr / normcx));
+        const dv3 wi = solid_angle_dir(smp, wc, cmax);
+        double t2;
+        int id2 = 0;
+        scene_isect(S, smp, xt, wi, t2, id2, false);
+        if (id2 == light) {
+            const dv3 Ls = scl(sph_rad(S, light), (phase * transmitance(xt, lp, sigma_t)));
+            const double prob = solid_angle_prob(cmax);
+            Li = add(Li, scl(scl(scl(Ls, (T * 1 / prob)), sigma_s), step));
+        } else {
+            Li = add(Li, mk(0, 0, 0));
+        }
+    }
+    return Li;
+}
+
+/* rayMarching, include/rayMarchingMethods.h:34-103: `steps` equal segments of the ray up to its first
+ * hit, solid-angle samples toward the hard-coded sphere 5; a light hit scores nothing (:48-51).
+ * x_new / idsource: the hit point and sphere (unchanged on a miss). */
+template <bool COUNT>
+VPT_DEV dv3 ray_marching_explicit(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, double sigma_t,
+                                  double sigma_s, double steps, dv3& x_new, int& idsource)
+{
+    double t;
+    int id = 0;
+    if (!scene_isect(S, smp, o, d, t, id, false)) return mk(0, 0, 0);
+    idsource = id;
+    const dv3 x = add(o, scl(d, t));
+    x_new = x;
+    if (S->sph[id].radiance[0] > 0) return mk(0, 0, 0);
+    return march_solid_angle(S, smp, o, d, x, steps, t / steps, 5, sigma_t, sigma_s);
+}
+
+/* rayMarching2, include/rayMarchingMethods.h:262-327 (estimator 7): steps of m.march_step toward
+ * sphere m.march_light by solid-angle sampling, plus the transmitted radiance of a light hit */
+template <bool COUNT>
+__device__ static dv3 trace_ray_marching2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d,
+                                          const Medium& m)
+{
+    const double step = m.march_step;
+    double t;
+    int id = 0;
+    if (!scene_isect(S, smp, o, d, t, id, false)) return mk(0, 0, 0);
+    const dv3 x = add(o, scl(d, t));
+    dv3 Lo = mk(0, 0, 0);
+    if (S->sph[id].radiance[0] > 0) Lo = scl(sph_rad(S, id), transmitance(o, x, m.sigma_a + m.sigma_s));
+    const dv3 Li = march_solid_angle(S, smp, o, d, x, t / step, step, m.march_light, m.sigma_a + m.sigma_s, m.sigma_s);
+    return add(Li, Lo);
+}
+
+/* rayMarchingGlobal, include/rayMarchingMethods.h:106-256 (estimator 8): up to 10 diffuse bounces,
+ * each a solid-angle sample toward sphere 5 and a cosine-sampled ray marched by rayMarching in
+ * m.march_step segments, then the camera ray marched from the last hit point.  As written: Ld keeps
+ * its value when the light sample misses (:169); every bounce's transmittance runs from the camera
+ * origin to the current x (:195). */
+template <bool COUNT>
+__device__ static dv3 trace_ray_marching_global(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d,
+                                                const Medium& m)
+{
+    const double sigma_s = m.sigma_s, segmentos = m.march_step;
+    const double sigma_t = m.sigma_a + m.sigma_s;
+    double t;
+    int id = 0;
+    if (!scene_isect(S, smp, o, d, t, id, false)) return mk(0, 0, 0);
+    dv3 x = add(o, scl(d, t));
+    dv3 Lo = mk(0, 0, 0);
+    if (S->sph[id].radiance[0] > 0) return scl(sph_rad(S, id), transmitance(o, x, sigma_t));
+    dv3 fs = mk(1, 1, 1), Ld = mk(0, 0, 0);
+    double factor = 1;
+    const dv3 l5 = sph_p(S, 5);
+    const double r5 = S->sph[5].r;
+    for (int i = 0; i < 10; i++) {
+        if (COUNT) smp.cnt.iterations++;
+        const dv3 fr = scl(sph_c(S, id), (1 / VPT_PI));
+        const dv3 n = nrm(sub(x, sph_p(S, id)));
+        dv3 wc = sub(l5, x);
+        const double normcx = vm_sqrt(dot(wc, wc));
+        wc = scl(wc, (1 / normcx));
+        const double cmax = vm_sqrt(1 - (r5 / normcx) * (r5 / normcx));
+        const dv3 wi = solid_angle_dir(smp, wc, cmax);
+        double t_aux;
+        int id_aux = 0;
+        scene_isect(S, smp, x, wi, t_aux, id_aux, false);
+        if (id_aux == 5) {
+            const dv3 Le = scl(sph_rad(S, 5), transmitance(x, l5, sigma_t));
+            Ld = scl(scl(mul(Le, fr), (1 / solid_angle_prob(cmax))), dot(n, wi));
+        }
+        const dv3 wray = cosine_hemispheric(smp, n);
+        const double prob = hemi_cosine_prob(dot(n, wray));
+        dv3 x_new = mk(0, 0, 0);
+        const dv3 Lm = ray_marching_explicit(S, smp, x, wray, sigma_t, sigma_s, segmentos, x_new, id);
+        Ld = add(Ld, scl(scl(mul(Lm, fr), dot(n, wray)), (1 / prob)));
+        Lo = add(Lo, scl(scl(mul(Ld, fs), transmitance(o, x, sigma_t)), factor));
+        if (Lm.x == 0 && Lm.y == 0 && Lm.z == 0) return Lo;
+        fs = mul(fs, fr);
+        factor = factor * dot(n, wray) * (1 / (prob));
+        x = x_new;
+    }
+    const dv3 Li = march_solid_angle(S, smp, o, d, x, segmentos, t / segmentos, 5, sigma_t, sigma_s);
+    return add(Li, Lo);
+}
+
+/* punctualVolumetric, include/rayMarchingMethods.h:12-31: single scattering at x from the centre of
+ * sphere idsource (visibilityVPT, multipleT); no draw */
+template <bool COUNT>
+VPT_DEV dv3 punctual_volumetric(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int idsource, dv3 x, double phase,
+                                double sigma_t, double sigma_s)
+{
+    const dv3 light = sph_p(S, idsource);
+    if (visibility(S, smp, light, x, true, S->sph[idsource].r, S->geo[idsource].mat3)) {
+        dv3 Le = sph_rad(S, idsource);
+        const double distanceLight = dot(sub(light, x), sub(light, x));
+        Le = scl(Le, (1 / distanceLight));
+        const dv3 Ls = scl(scl(Le, phase), multiple_t(S, smp, x, light, sigma_t));
+        return scl(Ls, sigma_s);
+    }
+    return mk(0, 0, 0);
+}
+
 /* One camera sample, sequentially (the reference's per-sample call; used by vpt_trace_batch). */
 template <int EST, bool COUNT>
 __device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, const Medium& m)
@@ -1262,6 +1398,14 @@ __device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT
         return trace_surface_pt<COUNT>(S, smp, o, d);
     } else if constexpr (EST == 6) {
         return trace_ray_marching<COUNT>(S, smp, o, d, m);
+    } else if constexpr (EST == 7) {
+        return trace_ray_marching2<COUNT>(S, smp, o, d, m);
+    } else if constexpr (EST == 8) {
+        return trace_ray_marching_global<COUNT>(S, smp, o, d, m);
+    } else if constexpr (EST == 9) {  /* rayMarching: the Color it returns (sigma_t = sigma_a + sigma_s) */
+        dv3 x_new = mk(0, 0, 0);
+        int idsource = 0;
+        return ray_marching_explicit<COUNT>(S, smp, o, d, m.sigma_a + m.sigma_s, m.sigma_s, m.march_step, x_new, idsource);
     } else {
         Path p;
         p.o = o;

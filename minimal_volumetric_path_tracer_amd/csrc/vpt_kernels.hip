@@ -273,6 +273,47 @@ __global__ __launch_bounds__(256) void trace_batch_kernel(const vpt_ray* __restr
     out_states[i] = smp.X;
 }
 
+/* punctualVolumetric (include/rayMarchingMethods.h:12-31) at n points */
+__global__ __launch_bounds__(256) void punctual_kernel(int idsource, const double* __restrict__ x, int n, double phase,
+                                                       double sigma_t, double sigma_s, const DevScene* __restrict__ S,
+                                                       double* out)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Sampler<false> smp;
+    smp.X = 0;
+    smp.g = 0;
+    const dv3 L = punctual_volumetric(S, smp, idsource, ld3(x + 3 * i), phase, sigma_t, sigma_s);
+    out[3 * i] = L.x;
+    out[3 * i + 1] = L.y;
+    out[3 * i + 2] = L.z;
+}
+
+/* rayMarching (include/rayMarchingMethods.h:34-103) with its out-parameters, one ray per lane */
+__global__ __launch_bounds__(256) void ray_marching_kernel(const vpt_ray* __restrict__ rays,
+                                                           const uint64_t* __restrict__ states, int n, double sigma_t,
+                                                           double sigma_s, double steps, const DevScene* __restrict__ S,
+                                                           double* out, double* x_new, int* idsource,
+                                                           uint64_t* out_states)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Sampler<false> smp;
+    smp.X = states[i] & 0xFFFFFFFFFFFFull;
+    smp.g = 0;
+    dv3 xn = ld3(x_new + 3 * i);
+    int id = idsource[i];
+    const dv3 L = ray_marching_explicit(S, smp, ld3(rays[i].o), ld3(rays[i].d), sigma_t, sigma_s, steps, xn, id);
+    out[3 * i] = L.x;
+    out[3 * i + 1] = L.y;
+    out[3 * i + 2] = L.z;
+    x_new[3 * i] = xn.x;
+    x_new[3 * i + 1] = xn.y;
+    x_new[3 * i + 2] = xn.z;
+    idsource[i] = id;
+    out_states[i] = smp.X;
+}
+
 __global__ void math_probe_kernel(int fn, const double* x, const double* y, double* out, int n)
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -364,14 +405,21 @@ static int check_medium(const vpt_medium* m)
     return VPT_OK;
 }
 
-/* rayMarching3's step and light (estimator 6 only): the light must be a sphere of the scene */
+/* the ray-marching estimators' parameters: march_step (the step of rayMarching3 / rayMarching2, the
+ * segment count of rayMarchingGlobal / rayMarching) finite and > 0; march_light (6, 7) a sphere of
+ * the scene; rayMarchingGlobal and rayMarching read the hard-coded sphere 5
+ * (include/rayMarchingMethods.h:64,153), so the scene needs at least 6 spheres */
 static int check_march(const vpt_context* ctx, const vpt_medium* m)
 {
-    if (m->estimator != VPT_RAY_MARCHING) return VPT_OK;
+    if (m->estimator < VPT_RAY_MARCHING) return VPT_OK;
     if (!is_finite(m->march_step) || !(m->march_step > 0))
         return vpt_fail(VPT_E_INVALID, "march_step must be finite and > 0");
-    if (m->march_light < 0 || m->march_light >= ctx->h_scene.n)
+    if ((m->estimator == VPT_RAY_MARCHING || m->estimator == VPT_RAY_MARCHING_SA) &&
+        (m->march_light < 0 || m->march_light >= ctx->h_scene.n))
         return vpt_fail(VPT_E_INVALID, "march_light %d is not a sphere of the scene (%d)", m->march_light, ctx->h_scene.n);
+    if ((m->estimator == VPT_RAY_MARCHING_GLOBAL || m->estimator == VPT_RAY_MARCHING_EXPLICIT) && ctx->h_scene.n < 6)
+        return vpt_fail(VPT_E_INVALID, "rayMarchingGlobal / rayMarching sample sphere 5: the scene has %d spheres",
+                        ctx->h_scene.n);
     return VPT_OK;
 }
 
@@ -477,7 +525,7 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         return VPT_OK;
     }
     if constexpr (!COUNT && EST < 5) return launch_pool<EST, FB>(ctx, K, stream);
-    if constexpr (EST >= 5) {  /* iterativePathTracer, rayMarching3: one lane per pixel, samples summed in order */
+    if constexpr (EST >= 5) {  /* iterativePathTracer, ray marching: one lane per pixel, samples summed in order */
         dim3 grid((unsigned)((K.w + 15) / 16), (unsigned)((K.shard_rows + 15) / 16));
         render_kernel_simple<EST, COUNT, FB><<<grid, dim3(256), 0, stream>>>(K, S);
         HIP_OK(hipGetLastError());
@@ -598,6 +646,9 @@ static int launch_render(vpt_context* ctx, KParams K, hipStream_t stream)
         VPT_LAUNCH_EST(4)
         VPT_LAUNCH_EST(5)
         VPT_LAUNCH_EST(6)
+        VPT_LAUNCH_EST(7)
+        VPT_LAUNCH_EST(8)
+        VPT_LAUNCH_EST(9)
     }
 #undef VPT_LAUNCH_EST
     return vpt_fail(VPT_E_INVALID, "unknown estimator %d", K.est);
@@ -778,7 +829,10 @@ int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, 
         case 3: trace_batch_kernel<3><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         case 4: trace_batch_kernel<4><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         case 5: trace_batch_kernel<5><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
-        default: trace_batch_kernel<6><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        case 6: trace_batch_kernel<6><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        case 7: trace_batch_kernel<7><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        case 8: trace_batch_kernel<8><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
+        default: trace_batch_kernel<9><<<grid, block>>>(dr, ds, n, mm, m->hg_g, ctx->d_scene, dout, dso); break;
         }
         e = hipGetLastError();
     }
@@ -789,6 +843,78 @@ int vpt_trace_batch(vpt_context* ctx, const vpt_medium* m, const vpt_ray* rays, 
     (void)hipFree(dso);
     (void)hipFree(dout);
     if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_trace_batch: %s", hipGetErrorString(e));
+    return VPT_OK;
+}
+
+int vpt_punctual_volumetric(vpt_context* ctx, int idsource, const double* x, int n, double phase, double sigma_t,
+                            double sigma_s, double* out_rgb)
+{
+    vpt_clear_error();
+    if (!ctx || !x || !out_rgb || n < 0) return vpt_fail(VPT_E_INVALID, "vpt_punctual_volumetric: bad arguments");
+    if (!ctx->has_scene) return vpt_fail(VPT_E_INVALID, "no scene set (vpt_set_scene)");
+    if (idsource < 0 || idsource >= ctx->h_scene.n)
+        return vpt_fail(VPT_E_INVALID, "idsource %d is not a sphere of the scene (%d)", idsource, ctx->h_scene.n);
+    if (n == 0) return VPT_OK;
+    HIP_OK(hipSetDevice(ctx->device));
+    double *dx = nullptr, *dout = nullptr;
+    const size_t b = sizeof(double) * 3 * (size_t)n;
+    hipError_t e = hipMalloc((void**)&dx, b);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, b);
+    if (e == hipSuccess) e = hipMemcpy(dx, x, b, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        punctual_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256)>>>(idsource, dx, n, phase, sigma_t, sigma_s,
+                                                                           ctx->d_scene, dout);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out_rgb, dout, b, hipMemcpyDeviceToHost);
+    (void)hipFree(dx);
+    (void)hipFree(dout);
+    if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_punctual_volumetric: %s", hipGetErrorString(e));
+    return VPT_OK;
+}
+
+int vpt_ray_marching_batch(vpt_context* ctx, double sigma_t, double sigma_s, double steps, const vpt_ray* rays,
+                           const uint64_t* states, int n, double* out_rgb, double* x_new, int32_t* idsource,
+                           uint64_t* out_states)
+{
+    vpt_clear_error();
+    if (!ctx || !rays || !states || !out_rgb || !x_new || !idsource || n < 0)
+        return vpt_fail(VPT_E_INVALID, "vpt_ray_marching_batch: bad arguments");
+    if (!ctx->has_scene) return vpt_fail(VPT_E_INVALID, "no scene set (vpt_set_scene)");
+    if (ctx->h_scene.n < 6) return vpt_fail(VPT_E_INVALID, "rayMarching samples sphere 5: the scene has %d spheres", ctx->h_scene.n);
+    if (!is_finite(steps) || !(steps > 0)) return vpt_fail(VPT_E_INVALID, "steps must be finite and > 0");
+    if (n == 0) return VPT_OK;
+    HIP_OK(hipSetDevice(ctx->device));
+    vpt_ray* dr = nullptr;
+    uint64_t *ds = nullptr, *dso = nullptr;
+    double *dout = nullptr, *dxn = nullptr;
+    int* did = nullptr;
+    hipError_t e = hipMalloc((void**)&dr, sizeof(vpt_ray) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc((void**)&ds, sizeof(uint64_t) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc((void**)&dso, sizeof(uint64_t) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * 3 * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc((void**)&dxn, sizeof(double) * 3 * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc((void**)&did, sizeof(int) * (size_t)n);
+    if (e == hipSuccess) e = hipMemcpy(dr, rays, sizeof(vpt_ray) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(ds, states, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dxn, x_new, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(did, idsource, sizeof(int) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        ray_marching_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256)>>>(dr, ds, n, sigma_t, sigma_s, steps,
+                                                                               ctx->d_scene, dout, dxn, did, dso);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out_rgb, dout, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(x_new, dxn, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(idsource, did, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && out_states) e = hipMemcpy(out_states, dso, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(dr);
+    (void)hipFree(ds);
+    (void)hipFree(dso);
+    (void)hipFree(dout);
+    (void)hipFree(dxn);
+    (void)hipFree(did);
+    if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_ray_marching_batch: %s", hipGetErrorString(e));
     return VPT_OK;
 }
 

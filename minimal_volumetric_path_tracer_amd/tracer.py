@@ -24,12 +24,14 @@ import numpy as np
 
 from . import _lib
 from ._lib import (EXPLICIT_EQUIANGULAR, EXPLICIT_FREE, FB_F32, FB_F64, FREE_FLIGHT, IMPLICIT_FREE, MIS_EQUIANGULAR,
-                   RAY_DTYPE, RAY_MARCHING, SPHERE_DTYPE, SURFACE_PT, check, lib)
+                   RAY_DTYPE, RAY_MARCHING, RAY_MARCHING_EXPLICIT, RAY_MARCHING_GLOBAL, RAY_MARCHING_SA, SPHERE_DTYPE,
+                   SURFACE_PT, check, lib)
 
 ESTIMATORS = {"ff": FREE_FLIGHT, "free_flight": FREE_FLIGHT, "mis": MIS_EQUIANGULAR, "mis_equiangular": MIS_EQUIANGULAR,
               "explicit_free": EXPLICIT_FREE, "implicit_free": IMPLICIT_FREE, "explicit": EXPLICIT_EQUIANGULAR,
               "explicit_equiangular": EXPLICIT_EQUIANGULAR, "surface_pt": SURFACE_PT, "path_tracer": SURFACE_PT,
-              "ray_marching": RAY_MARCHING}
+              "ray_marching": RAY_MARCHING, "ray_marching_sa": RAY_MARCHING_SA, "ray_marching_global": RAY_MARCHING_GLOBAL,
+              "ray_marching_explicit": RAY_MARCHING_EXPLICIT}
 
 
 def Sphere(r, p, c=(0, 0, 0), radiance=(0, 0, 0), material=0, eta=(0, 0, 0), kappa=(0, 0, 0), alpha=0.0) -> np.ndarray:
@@ -79,8 +81,9 @@ class RenderConfig:
     band_stride: int = 1
     band_offset: int = 0
     chunk_spp: int = 0          # 0 = auto (min(spp, 32), the last 64 samples tapered); 1 or >= spp = the reference's sequential sum
-    march_step: float = 0.1     # rayMarching3 (estimator "ray_marching") only: step (src/rt.cpp:791)
-    march_light: int = 7        # rayMarching3 only: light sphere index (src/rt.cpp:791)
+    march_step: float = 0.1     # ray marching: step (rayMarching3 / rayMarching2, src/rt.cpp:791) or segments
+                                # (rayMarchingGlobal / rayMarching)
+    march_light: int = 7        # rayMarching3 / rayMarching2: light sphere index (src/rt.cpp:791)
 
     def params(self) -> _lib.vpt_params:
         p = _lib.vpt_params()
@@ -195,6 +198,43 @@ class Tracer:
     def rayMarching3(self, rays, states, sigma_a, sigma_s, step, idsource):
         """Batched include/rayMarchingMethods.h:330 (src/rt.cpp:791 passes 0.001, 0.0125, 0.1, 7)."""
         return self.trace("ray_marching", rays, states, sigma_a, sigma_s, march_step=step, march_light=idsource)
+
+    def rayMarching2(self, rays, states, sigma_a, sigma_s, step, idsource):
+        """Batched include/rayMarchingMethods.h:262."""
+        return self.trace("ray_marching_sa", rays, states, sigma_a, sigma_s, march_step=step, march_light=idsource)
+
+    def rayMarchingGlobal(self, rays, states, sigma_a, sigma_s, segmentos):
+        """Batched include/rayMarchingMethods.h:106 (samples the hard-coded sphere 5)."""
+        return self.trace("ray_marching_global", rays, states, sigma_a, sigma_s, march_step=segmentos)
+
+    def rayMarching(self, rays, states, sigma_t, sigma_s, steps, x_new=None, idsource=None):
+        """Batched include/rayMarchingMethods.h:34 with its reference parameters: returns
+        (Color, x_new, idsource, end states); x_new / idsource are kept on a miss (inputs default
+        to 0 / -1)."""
+        r = np.ascontiguousarray(rays, dtype=RAY_DTYPE)
+        s = np.ascontiguousarray(states, dtype=np.uint64)
+        if len(r) != len(s):
+            raise ValueError("rays and states must have the same length")
+        xn = np.zeros((len(r), 3))
+        if x_new is not None:
+            xn[:] = x_new
+        ids = np.full(len(r), -1, dtype=np.int32)
+        if idsource is not None:
+            ids[:] = idsource
+        out = np.zeros((len(r), 3))
+        st = np.zeros(len(r), dtype=np.uint64)
+        check(lib().vpt_ray_marching_batch(self._ctx, float(sigma_t), float(sigma_s), float(steps), r.ctypes.data,
+                                           s.ctypes.data, len(r), out.ctypes.data, xn.ctypes.data, ids.ctypes.data,
+                                           st.ctypes.data))
+        return out, xn, ids, st
+
+    def punctualVolumetric(self, idsource: int, x: np.ndarray, phase: float, sigma_t: float, sigma_s: float) -> np.ndarray:
+        """include/rayMarchingMethods.h:12 at every point of x (n x 3) -> (n x 3) Colors."""
+        xs = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float64)
+        out = np.zeros_like(xs)
+        check(lib().vpt_punctual_volumetric(self._ctx, int(idsource), xs.ctypes.data, len(xs), float(phase),
+                                            float(sigma_t), float(sigma_s), out.ctypes.data))
+        return out
 
     def math_probe(self, fn: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float64)

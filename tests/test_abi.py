@@ -29,7 +29,7 @@ def test_exports_every_declared_symbol():
         assert hasattr(L, n), n
     bound = {p[0] for p in _lib.PROTOTYPES}
     assert bound == set(names), set(names) ^ bound
-    assert vpt.lib().vpt_abi_version() == 2
+    assert vpt.lib().vpt_abi_version() == 3
 
 
 def test_struct_layouts():

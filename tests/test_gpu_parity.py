@@ -549,3 +549,105 @@ def test_baseline_configs_vs_oracle(gpu_tracer, orc_vm, name, w, h, spp, kw):
     g = gpu_tracer.render(width=w, height=h, spp=spp, seed=SEED + 17, fp64=True, **kw)
     assert bitwise_equal(g, ref).all(), (name, np.abs(g - ref).max())
     assert np.isfinite(g).all() and g.max() > 0, name  # light reaches the camera (dense: sigma_t 0.03)
+
+
+# ---------------------------------------------------------------- estimators 7-9: rayMarching2,
+# rayMarchingGlobal, rayMarching (include/rayMarchingMethods.h:262, :106, :34) and punctualVolumetric (:12)
+def _e789_keys():
+    path = os.path.join(GOLDEN, "samples_e789.npz")
+    return sorted(k[:-len("__march")] for k in np.load(path).files if k.endswith("__march"))
+
+
+E789_NAMES = {7: "ray_marching_sa", 8: "ray_marching_global", 9: "ray_marching_explicit"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _e789_keys())
+def test_trace_batch_vs_reference_bitwise_e789(gpu_tracer, orc_vm, samples_e789, case):
+    """per sample: the reference's own values and end states, bit for bit (glibc-exact device libm)"""
+    sc = samples_e789[f"{case}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    est, step, light = samples_e789[f"{case}__march"]
+    est, light = int(est), int(light)
+    k = f"{case}__"
+    rays, st = samples_e789[k + "ray"], samples_e789[k + "state1"]
+    if est == 7:
+        L, s = gpu_tracer.rayMarching2(_rays(rays), st, 0.001, 0.0125, step, light)
+    elif est == 8:
+        L, s = gpu_tracer.rayMarchingGlobal(_rays(rays), st, 0.001, 0.0125, step)
+    else:
+        L, s = gpu_tracer.trace(E789_NAMES[9], _rays(rays), st, 0.001, 0.0125, march_step=step)
+    assert np.array_equal(s, samples_e789[k + "state2"])
+    same = bitwise_equal(L, samples_e789[k + "L"])
+    assert same.all(), f"{(~same.all(1)).sum()} of {len(L)} samples differ from the reference"
+    Lo, so = orc_vm.trace(est, rays, st, 0.001, 0.0125, march_step=step, march_light=light)
+    assert bitwise_equal(L, Lo).all() and np.array_equal(s, so)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _e789_keys())
+def test_render_vs_reference_bitwise_e789(gpu_tracer, samples_e789, case):
+    sc = samples_e789[f"{case}__scene"].view(vpt.SPHERE_DTYPE)
+    gpu_tracer.set_scene(sc)
+    est, step, light = samples_e789[f"{case}__march"]
+    g = gpu_tracer.render(width=16, height=16, spp=2, estimator=E789_NAMES[int(est)], sigma_a=0.001, sigma_s=0.0125,
+                          march_step=float(step), march_light=int(light), seed=SEED, fp64=True)
+    assert bitwise_equal(g, samples_e789[f"{case}__fb16x16x2"]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("est", [7, 8, 9])
+def test_count_work_matches_oracle_e789(gpu_tracer, orc_vm, est):
+    from scenes import ALT_SCENES
+    sc = ALT_SCENES["alt_area_light"]()
+    gpu_tracer.set_scene(sc.view(vpt.SPHERE_DTYPE))
+    orc_vm.set_scene(sc)
+    step = 0.75 if est == 7 else 5.0
+    cfg = vpt.RenderConfig(width=16, height=12, spp=2, estimator=E789_NAMES[est], march_step=step, march_light=5,
+                           sigma_a=0.001, sigma_s=0.0125, seed=9)
+    t, it = gpu_tracer.count_work(cfg)
+    _, c = orc_vm.render(16, 12, 2, est, 0.001, 0.0125, seed=9, counters=True, chunk=2, march_step=step, march_light=5)
+    assert (t, it) == (c.tests, c.iterations) and it > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["default", "mat3", "point_lights"])
+def test_punctual_volumetric_vs_reference_bitwise(gpu_tracer, samples_e789, scene):
+    gpu_tracer.set_scene(samples_e789[f"pv_{scene}__scene"].view(vpt.SPHERE_DTYPE))
+    ids, xs, want = samples_e789[f"pv_{scene}__id"], samples_e789[f"pv_{scene}__x"], samples_e789[f"pv_{scene}__out"]
+    got = np.concatenate([gpu_tracer.punctualVolumetric(int(i), xs[ids == i], 1 / (4 * np.pi), 0.0135, 0.0125)
+                          for i in np.unique(ids)])
+    order = np.concatenate([np.nonzero(ids == i)[0] for i in np.unique(ids)])
+    assert bitwise_equal(got, want[order]).all()
+
+
+@pytest.mark.gpu
+def test_ray_marching_out_parameters_vs_reference(gpu_tracer, samples_e789):
+    from scenes import ALT_SCENES
+    gpu_tracer.set_scene(ALT_SCENES["alt_area_light"]().view(vpt.SPHERE_DTYPE))
+    rays, s1 = samples_e789["rmx__ray"], samples_e789["rmx__state1"]
+    L, xn, ids, s2 = gpu_tracer.rayMarching(_rays(rays), s1, 0.0135, 0.0125, 7.0, x_new=samples_e789["rmx__xin"],
+                                            idsource=-1)
+    want = samples_e789["rmx__out"]
+    assert bitwise_equal(L, want[:, :3]).all() and bitwise_equal(xn, want[:, 3:]).all()
+    assert np.array_equal(ids, samples_e789["rmx__id"]) and np.array_equal(s2, samples_e789["rmx__state2"])
+    assert (ids == -1).any() and (ids >= 0).any()
+
+
+@pytest.mark.gpu
+def test_ray_marching_789_invalid_arguments(gpu_tracer):
+    gpu_tracer.set_scene(vpt.default_scene())
+    for est in ("ray_marching_sa", "ray_marching_global", "ray_marching_explicit"):
+        for kw in (dict(march_step=0.0), dict(march_step=float("inf"))):
+            with pytest.raises(vpt.VPTError):
+                gpu_tracer.render(width=8, height=8, spp=1, estimator=est, **kw)
+    with pytest.raises(vpt.VPTError):
+        gpu_tracer.render(width=8, height=8, spp=1, estimator="ray_marching_sa", march_light=10)
+    gpu_tracer.set_scene(vpt.default_scene()[[0, 1, 2, 3, 7]])  # sphere 5 (hard-coded by rayMarching) missing
+    for est in ("ray_marching_global", "ray_marching_explicit"):
+        with pytest.raises(vpt.VPTError):
+            gpu_tracer.render(width=8, height=8, spp=1, estimator=est, march_step=4.0)
+    with pytest.raises(vpt.VPTError):
+        gpu_tracer.punctualVolumetric(7, np.zeros((1, 3)), 0.1, 0.01, 0.01)
+    gpu_tracer.set_scene(vpt.default_scene())
