@@ -512,6 +512,18 @@ static int launch_wave(vpt_context* ctx, KParams K, hipStream_t stream);
 template <int EST, int FB>
 static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream);
 
+/* log2(v) when v is a power of two, else -1 (PoolParams shift fast paths; VPT_POW2=0: always -1, A/B) */
+#ifndef VPT_POW2
+#define VPT_POW2 1
+#endif
+static int log2_exact(int64_t v)
+{
+    if (!VPT_POW2 || v <= 0 || (v & (v - 1)) != 0) return -1;
+    int k = 0;
+    while ((v >> k) != 1) ++k;
+    return k;
+}
+
 template <int EST, bool COUNT, int FB>
 static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
 {
@@ -555,6 +567,11 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         Q.lay = vpt_chunks(K.spp, K.chunk, K.taper);
         Q.nch = Q.lay.n;
         Q.level_units = (unsigned)K.tiles_x * (unsigned)K.tiles_y * 64u;
+        Q.sh_lu = log2_exact((int64_t)Q.level_units);
+        Q.sh_tx = log2_exact(K.tiles_x);
+        Q.sh_br = log2_exact(K.band_rows);
+        Q.sh_bs = log2_exact(K.band_stride);
+        Q.sh_c = log2_exact(Q.lay.C);
         const uint64_t units = (uint64_t)K.tiles_x * (uint64_t)K.tiles_y * 64u * (uint64_t)Q.nch;
         if (units >= 0xFFFFFFFFull) return vpt_fail(VPT_E_INVALID, "too many work units (%llu)", (unsigned long long)units);
         Q.seed = K.seed;

@@ -145,11 +145,18 @@ struct PoolParams {
     unsigned unit0;
     uint64_t seed;
     double o[3], d[3], cx[3], cy[3];
+    /* log2 of level_units, tiles_x, band_rows, band_stride and the chunk size C when they are powers of
+     * two, else -1: the unit decode and the partial's address divide by them (a u32 division is ~15
+     * VALU instructions; every lane of a wave runs it when one lane takes or finishes a unit) */
+    int sh_lu, sh_tx, sh_br, sh_bs, sh_c;
     double* partials;       /* nch * rows * w * 3: chunk-major, so the units of one chunk level (handed
                              * out together, 8x8 tiles) write neighbouring 24-B records that merge into
                              * whole lines in L2 (pixel-major wrote 24 B per 128-B line: 2x the WRITE_SIZE) */
     unsigned* queue;
 };
+
+/* a / d for a launch constant d = 2^sh (sh >= 0: a shift; the branch is uniform) */
+__device__ __forceinline__ unsigned udiv_p(unsigned a, unsigned d, int sh) { return sh >= 0 ? a >> sh : a / d; }
 
 /* work unit -> pixel and chunk.  Chunk-major: all units of chunk 0 (8x8 tiles in order, 64
  * consecutive units per tile), then chunk 1, ...; with the tapered layout the last units handed
@@ -163,13 +170,14 @@ __device__ __forceinline__ Unit decode_unit(const PoolParams& P, unsigned u)
 {
     u += P.unit0;
     Unit r;
-    const unsigned c = u / P.level_units, rem = u - c * P.level_units;
+    const unsigned c = udiv_p(u, P.level_units, P.sh_lu), rem = u - c * P.level_units;
     r.c = (int)c;
     const unsigned tile = rem >> 6, p = rem & 63u;
-    r.x = (int)(tile % (unsigned)P.tiles_x) * 8 + (int)(p & 7u);
-    const int lr = (int)(tile / (unsigned)P.tiles_x) * 8 + (int)(p >> 3);  /* row within the shard */
+    const unsigned ty = udiv_p(tile, (unsigned)P.tiles_x, P.sh_tx);
+    r.x = (int)(tile - ty * (unsigned)P.tiles_x) * 8 + (int)(p & 7u);
+    const int lr = (int)ty * 8 + (int)(p >> 3);  /* row within the shard */
     r.valid = r.x < P.w && lr < P.rows;
-    const int k = lr / P.band_rows, rr = lr - k * P.band_rows;
+    const int k = (int)udiv_p((unsigned)lr, (unsigned)P.band_rows, P.sh_br), rr = lr - k * P.band_rows;
     const int fr = (P.band_offset + k * P.band_stride) * P.band_rows + rr;  /* file row */
     r.y = P.h - 1 - fr;                                                       /* camera row */
     return r;
@@ -254,9 +262,10 @@ __device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t
 {
     const int x = (int)(t.pix & 0xFFFFu), y = (int)(t.pix >> 16);
     const int fr = P.h - 1 - y;
-    const int k = fr / P.band_rows, rr = fr - k * P.band_rows;
-    const int lr = ((k - P.band_offset) / P.band_stride) * P.band_rows + rr;
-    const int c = vpt_chunk_of_end(&P.lay, (int)t.c1);
+    const int k = (int)udiv_p((unsigned)fr, (unsigned)P.band_rows, P.sh_br), rr = fr - k * P.band_rows;
+    const int lr = (int)udiv_p((unsigned)(k - P.band_offset), (unsigned)P.band_stride, P.sh_bs) * P.band_rows + rr;
+    const int c = (int)t.c1 <= P.lay.head ? (int)udiv_p(t.c1 - 1u, (unsigned)P.lay.C, P.sh_c)  /* vpt_chunk_of_end */
+                                          : vpt_chunk_of_end(&P.lay, (int)t.c1);
     const size_t o = (((size_t)c * (size_t)P.rows + (size_t)lr) * (size_t)P.w + (size_t)x) * 3;
     P.partials[o] = t.acc.x;
     P.partials[o + 1] = t.acc.y;
@@ -334,7 +343,12 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                         t.pix = (unsigned)uu.x | ((unsigned)uu.y << 16);
                         t.key = vpt_stream_key(P.seed, (uint64_t)(P.h - 1 - uu.y) * (uint64_t)P.w + (uint64_t)uu.x);
                         int s0, s1;
-                        vpt_chunk_range(&P.lay, uu.c, &s0, &s1);
+                        if (uu.c < P.lay.n_head) {  /* vpt_chunk_range: a chunk of C */
+                            s0 = uu.c * P.lay.C;
+                            s1 = s0 + P.lay.C < P.lay.head ? s0 + P.lay.C : P.lay.head;
+                        } else {
+                            vpt_chunk_range(&P.lay, uu.c, &s0, &s1);
+                        }
                         t.i = (unsigned)s0;
                         t.c1 = (unsigned)s1;
                         t.in_path = false;
