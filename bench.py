@@ -60,6 +60,11 @@ CONFIGS = {
     "dense": dict(width=2048, height=2048, spp=4096, estimator="ff", sigma_a=0.003, sigma_s=0.027, max_depth=8),
     # BASELINE.json configs[4]: meant for --gpus 8 (137 G samples per image; ~4 s per step on 8 GPUs)
     "mis4k": dict(width=4096, height=4096, spp=8192, estimator="mis", sigma_a=0.001, sigma_s=0.009),
+    # the commented alternatives of main() (src/rt.cpp:791,793) on the one-lane-per-pixel kernel
+    # (throughput of estimators 5 and 6; parity cases, not bench lines of the driver)
+    "pt": dict(width=1024, height=1024, spp=64, estimator="surface_pt", sigma_a=0.001, sigma_s=0.009),
+    "march": dict(width=1024, height=768, spp=4, estimator="ray_marching", sigma_a=0.001, sigma_s=0.0125,
+                  march_step=0.1, march_light=8),
 }
 
 

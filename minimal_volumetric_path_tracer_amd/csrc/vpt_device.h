@@ -322,7 +322,16 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
 VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
 {
     double st, ct, sp, cp;
-    lm_dir_trig(c, phi, &st, &ct, &sp, &cp);
+    if (__ballot(c != 1.0) == 0) {
+        /* c == 1 in every lane (the cone toward a point light: cmax = sqrt(1 - 0) = 1 and
+         * (1 - e0) + e0 * 1 = 1 exactly): glibc's acos(1) = +0, sin(+0) = +0, cos(+0) = 1, so only
+         * the azimuth's sin and cos are evaluated -- the same bits */
+        st = 0.0;
+        ct = 1.0;
+        lm_sincos(phi, &sp, &cp);
+    } else {
+        lm_dir_trig(c, phi, &st, &ct, &sp, &cp);
+    }
     return nrm(from_local(n, st * cp, st * sp, ct));
 }
 
@@ -923,7 +932,9 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     dv3 wc = sub(lp, xt);
     double mag = vm_sqrt(dot(wc, wc));
     wc = scl(wc, (1 / mag));
-    double cmax = vm_sqrt(1 - lr / mag * (lr / mag));
+    /* a point light (LT == 1, lr = 0): 0 / mag is +0 for mag > 0 (mag >= 0 or NaN), NaN otherwise,
+     * so the cosine is 1 or NaN -- the same value without the division and the root */
+    double cmax = LT == 1 ? (mag > 0 ? 1.0 : __builtin_nan("")) : vm_sqrt(1 - lr / mag * (lr / mag));
     dv3 wl = solid_angle_dir(smp, wc, cmax);
     double prob_wl = solid_angle_prob(cmax);
     double tdist;
