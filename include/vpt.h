@@ -69,8 +69,8 @@ typedef enum {
     VPT_EXPLICIT_EQUIANGULAR = 4,  /* explicitVPTracerRecursive, vptShadeMethods.h:1014 */
     VPT_SURFACE_PT = 5,            /* iterativePathTracer, shadeMethods.h:104: surface-only path tracing (the
                                     * commented alternative at src/rt.cpp:793); sigma_a, sigma_s, hg_g and
-                                    * max_depth are ignored; renders sum each pixel's samples in the
-                                    * reference's sequential order (chunk_spp ignored) */
+                                    * max_depth are ignored; rendered by the task-pool kernel like 0-4
+                                    * (chunk_spp applies) */
     VPT_RAY_MARCHING = 6,          /* rayMarching3, rayMarchingMethods.h:330: constant-step marching toward the
                                     * light march_light (the commented alternative at src/rt.cpp:791, which
                                     * passes sigma_a 0.001, sigma_s 0.0125, step 0.1, light 7); draws nothing

@@ -1045,6 +1045,18 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
 #else
     const bool hit = scene_intersect(S, smp, p.o, p.d, t, id, false);
 #endif
+    if constexpr (EST == 5) {  /* iterativePathTracer (shadeMethods.h:115-125): nearest hit or end */
+        if (COUNT) smp.cnt.iterations++;
+        e.t = t;
+        e.id = id;
+        e.src = 0;
+        if (!hit) return EV_END;
+        if (S->sph[id].radiance[0] > 0) {  /* a light: the camera ray returns its radiance, a later hit ends */
+            if (p.depth < 1) p.L = sph_rad(S, id);
+            return EV_END;
+        }
+        return EV_SURF;
+    }
     if (!hit) t = VPT_MAXFLOAT;
     e.t = t;
     e.id = id;
@@ -1131,6 +1143,40 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
 
 /* medium event: single-scattering NEE toward the picked light, phase-function continuation.
  * LT: 1 point light, 0 not, -1 unknown (the pool kernel's medium rings are keyed by it) */
+/* One bounce of iterativePathTracer (include/shadeMethods.h:126-160) at the surface hit of event e,
+ * for the pool kernel: pLight for every r == 0 sphere in index order and MIS without transmittance
+ * (Ld = term + Ld), the roulette draw (q = 0.4, after the NEE: a killed path drops this vertex's Ld),
+ * then the BSDF continuation; Accum (p.L) += fs Ld factor, fs (p.beta) *= fs1, factor (carried in
+ * the event's pdf slot) *= cos / (prob 0.6).  Same operations as trace_surface_pt.  Returns true when
+ * the roulette ends the path.  MK: the hit sphere's material when the surface ring fixes it. */
+template <bool COUNT, int MK = -1>
+VPT_DEV bool surface_event_pt(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, Event& e)
+{
+    const double q = 0.4;
+    const double continueprob = 1.0 - q;
+    const int id = e.id;
+    const dv3 x = add(p.o, scl(p.d, e.t));
+    const dv3 nx = nrm(sub(x, sph_p(S, id)));
+    const double alpha = S->sph[id].alpha;
+    dv3 Ld = mk(0, 0, 0);
+    const int n = S->n;
+    for (int l = 0; l < n; ++l)  /* wave-uniform: scalar loads of the scene */
+        if (S->sph[l].r == 0) Ld = add(p_light<COUNT, MK>(S, smp, id, x, nx, p.d, l, alpha), Ld);
+    Ld = add(mis_v2<COUNT, MK, false>(S, smp, id, x, nx, p.d, alpha, 0.0), Ld);
+    if (smp.next() < q) return true;
+    double prob = 0;
+    dv3 wi = mk(0, 0, 0);
+    const dv3 fs1 = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, prob, id);
+    p.o = x;
+    p.d = wi;
+    const double cosine = dot(nx, wi);
+    p.L = add(p.L, scl(mul(p.beta, Ld), e.pdf));
+    p.beta = mul(p.beta, fs1);
+    e.pdf = e.pdf * cosine * (1 / (prob * continueprob));
+    p.depth++;
+    return false;
+}
+
 template <int EST, bool COUNT, int LT = -1>
 VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
                           const Medium& m)

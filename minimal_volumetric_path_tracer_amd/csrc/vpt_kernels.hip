@@ -536,8 +536,8 @@ static int launch_one(vpt_context* ctx, KParams K, hipStream_t stream)
         HIP_OK(hipGetLastError());
         return VPT_OK;
     }
-    if constexpr (!COUNT && EST < 5) return launch_pool<EST, FB>(ctx, K, stream);
-    if constexpr (EST >= 5) {  /* iterativePathTracer, ray marching: one lane per pixel, samples summed in order */
+    if constexpr (!COUNT && EST <= 5) return launch_pool<EST, FB>(ctx, K, stream);
+    if constexpr (EST >= 6) {  /* ray marching: one lane per pixel, samples summed in order */
         dim3 grid((unsigned)((K.w + 15) / 16), (unsigned)((K.shard_rows + 15) / 16));
         render_kernel_simple<EST, COUNT, FB><<<grid, dim3(256), 0, stream>>>(K, S);
         HIP_OK(hipGetLastError());

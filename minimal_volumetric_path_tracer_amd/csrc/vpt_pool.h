@@ -368,11 +368,17 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                 /* the first roulette draw (vptShadeMethods.h:1282, continue_path at depth 0) is the
                  * stream's third, after the jitter pair: decide it from the state three steps on;
                  * the jitter and the camera ray are built after the loop, for survivors only */
-                if (COUNT) smp.cnt.iterations++;
-                if (!(vpt_erand48_value(vpt_erand48_skip3(X0)) < 1 - 0.6)) {
+                if (EST == 5) {  /* iterativePathTracer draws no roulette before its first intersection */
                     t.X = X0;
                     t.in_path = true;
                     fresh = true;
+                } else {
+                    if (COUNT) smp.cnt.iterations++;
+                    if (!(vpt_erand48_value(vpt_erand48_skip3(X0)) < 1 - 0.6)) {
+                        t.X = X0;
+                        t.in_path = true;
+                        fresh = true;
+                    }
                 }
             }
         }
@@ -389,12 +395,13 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         smp.X = t.X;
         const double jx = smp.next();  /* x draw first */
         const double jy = smp.next();
-        (void)smp.next();  /* the roulette draw, decided above */
+        if (EST != 5) (void)smp.next();  /* the roulette draw, decided above */
         t.p.o = mk(P.o[0], P.o[1], P.o[2]);
         t.p.d = pool_camera_dir(P, jx, jy, (int)(t.pix & 0xFFFFu), (int)(t.pix >> 16));
         t.p.beta = mk(1, 1, 1);
         t.p.L = mk(0, 0, 0);
         t.p.depth = 0;
+        if (EST == 5) t.e.pdf = 1;  /* iterativePathTracer's `factor` rides in the event's pdf slot */
         t.X = smp.X;
     }
     const unsigned long long c1 = dbg_clock(dbg);
@@ -409,7 +416,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             result = R_A;
         } else if (ev == EV_SURF) {  /* (the implicit estimator, EST 3, picks no light) */
             const int sk = S->geo[t.e.id].skey;
-            result = R_S + (sk == 0 ? (EST == 3 ? 0 : S->geo[t.e.src].point) : sk);
+            result = R_S + (sk == 0 ? (EST == 3 || EST == 5 ? 0 : S->geo[t.e.src].point) : sk);
         } else {
             result = R_M + (EST == 3 ? 0 : S->geo[t.e.src].point);
             t.e.t = t.e.dist;  /* one slot (F_TD): stage M reads the sampled distance */
@@ -704,17 +711,23 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                 smp.X = t.X;
                 /* surface rings are keyed by material: diffuse (R_S, R_S+1), metal (R_S+2), other */
                 /* and by light kind: sphere light (R_S, R_M), point light (R_S + 1, R_M + 1) */
-                if (stage == 1) {
-                    if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m);
-                    else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
-                    else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
-                    else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
-                } else if (st == R_M) {
-                    medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
+                if constexpr (EST == 5) {  /* iterativePathTracer: the roulette is inside the bounce */
+                    if (st == R_S + 2) t.killed = surface_event_pt<COUNT, 1>(S, smp, t.p, t.e);
+                    else if (st == R_S) t.killed = surface_event_pt<COUNT, 0>(S, smp, t.p, t.e);
+                    else t.killed = surface_event_pt<COUNT, -1>(S, smp, t.p, t.e);
                 } else {
-                    medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
+                    if (stage == 1) {
+                        if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m);
+                        else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
+                        else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
+                        else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
+                    } else if (st == R_M) {
+                        medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
+                    } else {
+                        medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
+                    }
+                    t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
                 }
-                t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
                 t.X = smp.X;
             } else {
                 t.c1 = 0;

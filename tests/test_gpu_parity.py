@@ -426,7 +426,8 @@ def test_trace_batch_vs_reference_e5(gpu_tracer, samples_e5, scene):
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene", ["default", "big_light", "dielectric", "alt_open_space"])
 def test_render_vs_oracle_bitwise_e5(gpu_tracer, orc_vm, scene):
-    """renders sum a pixel's samples in the reference's order (chunk_spp is ignored for estimator 5)"""
+    """estimator 5 on the pool kernel: chunk sums like the other estimators (auto: spp <= 32 is one
+    chunk, the reference's order; explicit chunk_spp: uniform chunks), bit-exact vs the oracle's layout"""
     sc = _e5_scene(scene)
     gpu_tracer.set_scene(sc)
     orc_vm.set_scene(sc)
@@ -434,8 +435,18 @@ def test_render_vs_oracle_bitwise_e5(gpu_tracer, orc_vm, scene):
     for chunk in (0, 7):
         g = gpu_tracer.render(width=40, height=28, spp=20, estimator="surface_pt", seed=SEED, fp64=True,
                               chunk_spp=chunk)
-        assert bitwise_equal(g, o).all()
+        assert bitwise_equal(g, o if chunk == 0 else orc_vm.render(40, 28, 20, 5, seed=SEED, chunk=7)).all()
     assert np.abs(o).sum() > 0
+
+
+@pytest.mark.gpu
+def test_render_vs_oracle_bitwise_e5_tapered(gpu_tracer, orc_vm):
+    """70 spp: auto chunks of 32 with the tapered tail (csrc/vpt_chunks.h), as the oracle lays them out"""
+    sc = _e5_scene("default")
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    g = gpu_tracer.render(width=24, height=16, spp=70, estimator="surface_pt", seed=SEED, fp64=True)
+    assert bitwise_equal(g, orc_vm.render(24, 16, 70, 5, seed=SEED, chunk=None, threads=4)).all()
 
 
 @pytest.mark.gpu
