@@ -50,8 +50,12 @@ def main():
         wc = g("SQ_WAVE_CYCLES")
         if g("SQ_ACTIVE_INST_ANY"):
             der["wave_cycles_issuing_frac"] = g("SQ_ACTIVE_INST_ANY") / wc
+        # MI355X_MICROARCH.md: SQ_WAIT_ANY = wave parked (s_waitcnt / barrier / sleep), SQ_WAIT_INST_ANY =
+        # issue stall (dependency / pipe); with ACTIVE_INST_ANY they partition WAVE_CYCLES
+        if g("SQ_WAIT_ANY"):
+            der["wave_cycles_waitcnt_frac"] = g("SQ_WAIT_ANY") / wc
         if g("SQ_WAIT_INST_ANY"):
-            der["wave_cycles_waitcnt_frac"] = g("SQ_WAIT_INST_ANY") / wc
+            der["wave_cycles_issue_stall_frac"] = g("SQ_WAIT_INST_ANY") / wc
         if g("SQ_WAIT_INST_LDS"):
             der["wave_cycles_wait_lds_frac"] = g("SQ_WAIT_INST_LDS") / wc
     if g("SQ_INSTS_VALU") and g("SQ_WAVES"):
@@ -70,6 +74,8 @@ def main():
         der["hbm_write_bytes"] = g("WRITE_SIZE") * 1024
     if g("GRBM_GUI_ACTIVE"):
         der["effective_clock_ghz"] = g("GRBM_GUI_ACTIVE") / 8 / dispatch["duration_ns"]  # summed over 8 XCDs
+        if g("SQ_ACTIVE_INST_VALU"):  # quad-cycles of VALU issue summed over waves, per SIMD-cycle (1024 SIMDs)
+            der["simd_valu_busy_frac"] = 4 * g("SQ_ACTIVE_INST_VALU") / (1024 * g("GRBM_GUI_ACTIVE") / 8)
     if g("SQ_LEVEL_WAVES") and g("SQ_BUSY_CYCLES"):
         der["mean_resident_waves_per_se"] = g("SQ_LEVEL_WAVES") / g("SQ_BUSY_CYCLES")
     out = {"source": f"rocprofv3 --pmc <counters> --kernel-trace, one pass per counter group (scripts/pmc.sh), "
