@@ -420,7 +420,8 @@ def main() -> None:
                 "peak_no_fma": FP64_PEAK_TFLOPS / 2,
                 "frac_of_no_fma_peak": round(m["achieved"] / (FP64_PEAK_TFLOPS / 2), 5),
                 "traffic": pmc_traffic(prof),
-                "kernel": f"pool_kernel<{'FF' if c['estimator'] == 'ff' else 'MIS'}> + reduce_kernel (one launch pair)",
+                "kernel": (f"pool_kernel<{c['estimator']}> + reduce_kernel (one launch pair)"
+                           if c["estimator"] not in ("ray_marching",) else "render_kernel_simple (one lane per pixel)"),
                 "kernel_ms": round(kern_ms, 3),
                 "kernel_ms_from": "HIP events around each launch of the timed steps on their stream" if D == 1 else
                                   f"HIP events around {m['nevents']} serialized launches of the same render on one stream, "
@@ -441,6 +442,11 @@ def main() -> None:
         if world == 1 and not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(img, c, threads)
             res["cpu_baseline"]["port_per_sample_rng"] = cpu_port_check(img, c, threads, bands=4)
+            cb0 = res["cpu_baseline"]
+            # ratios of this line's value to the reference program (vs_baseline stays null: BASELINE.md
+            # holds no published number for this metric)
+            cb0["speedup_vs_measured"] = round(m["value"] / cb0["value"], 1)
+            cb0["speedup_vs_socket_estimate"] = round(m["value"] / cb0["socket_estimate"]["value"], 1)
         if ns is not None:
             cn = CONFIGS[NORTH_STAR]
             o = {"workload": workload_name(cn) + " (BASELINE.json configs[2])",
