@@ -202,7 +202,8 @@ int vpt_count_work(vpt_context* ctx, const vpt_params* p, uint64_t* tests, uint6
 uint64_t vpt_stream_state(uint64_t seed, uint64_t pixel_idx, uint64_t sample);
 
 /* Evaluates the device math library on the GPU: fn 0 sqrt, 1 exp, 2 log, 3 sin, 4 cos, 5 tan,
- * 6 atan, 7 acos, 8 atan2(x, y), 9 x / y.  Host arrays, synchronous (parity tests). */
+ * 6 atan, 7 acos, 8 atan2(x, y), 9 x / y, 10 / 11 sin / cos of acos(x), 12 1 / sqrt(x) (the
+ * normalisation's reciprocal).  Host arrays, synchronous (parity tests). */
 int vpt_math_probe(vpt_context* ctx, int fn, const double* x, const double* y, double* out, int n);
 
 /* PPM writer of main() (src/rt.cpp:812-820): clamp to [0,1] (src/rt.cpp:803), gamma 1/2.2,

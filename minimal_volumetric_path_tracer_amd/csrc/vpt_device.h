@@ -76,7 +76,7 @@ VPT_DEV dv3 scl(dv3 a, double s) { return dv3{a.x * s, a.y * s, a.z * s}; }
 VPT_DEV dv3 mul(dv3 a, dv3 b) { return dv3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 VPT_DEV double dot(dv3 a, dv3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 VPT_DEV dv3 cross(dv3 a, dv3 b) { return dv3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
-VPT_DEV dv3 nrm(dv3 a) { return scl(a, 1.0 / vm_sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); }
+VPT_DEV dv3 nrm(dv3 a) { return scl(a, vm_inv_sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); }  /* 1.0 / sqrt(|a|^2) */
 
 struct Counters {
     uint64_t tests;

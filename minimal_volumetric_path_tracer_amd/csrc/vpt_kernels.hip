@@ -329,6 +329,7 @@ __global__ void math_probe_kernel(int fn, const double* x, const double* y, doub
     case 6: r = lm_atan(a); break;
     case 7: r = lm_acos(a); break;
     case 8: r = lm_atan2(a, b); break;
+    case 12: r = vm_inv_sqrt(a); break;  /* 1.0 / sqrt(a) (nrm) */
     case 10:
     case 11: {
         double sv, cv;

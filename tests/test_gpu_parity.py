@@ -55,6 +55,27 @@ def test_device_sqrt_div_correctly_rounded(gpu_tracer, orc):
     assert bitwise_equal(gpu_tracer.math_probe(9, x, y), x / y).all()
 
 
+def test_device_inv_sqrt_exact(gpu_tracer):
+    """vm_inv_sqrt (nrm's 1.0 / sqrt(|a|^2): the square root and the division sequences without their
+    scaling / fix-up steps inside [2^-767, DBL_MAX]) == 1.0 / np.sqrt(x) bit for bit, across the
+    exponent range, at the fast path's ends, on exact squares and their neighbours, and on specials"""
+    rng = np.random.default_rng(12)
+    x = np.abs(rng.normal(size=400000)) * 10.0 ** rng.integers(-320, 309, 400000)
+    lo = 2.0 ** -767
+    edges = np.array([lo, np.nextafter(lo, 0), np.nextafter(lo, 1), 2.0 ** -1022, 5e-324, 1e-310,
+                      np.finfo(np.float64).max, np.nextafter(np.finfo(np.float64).max, 0), 0.0, -0.0, -1.0,
+                      np.inf, -np.inf, np.nan, 1.0, 4.0, 0.25, 2.0, 0.5])
+    sq = (rng.integers(1, 1 << 26, 20000).astype(np.float64)) ** 2 * 2.0 ** rng.integers(-600, 600, 20000)
+    near = np.concatenate([sq, np.nextafter(sq, 0), np.nextafter(sq, np.inf)])
+    unit = 1.0 + rng.uniform(-1e-6, 1e-6, 100000)  # |a|^2 of nearly unit vectors (the path's common case)
+    x = np.concatenate([x, edges, near, unit])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        want = 1.0 / np.sqrt(x)
+    got = gpu_tracer.math_probe(12, x)
+    same = bitwise_equal(got, want)
+    assert same.all(), f"{(~same).sum()} differ, e.g. x={x[~same][:3]} got={got[~same][:3]} want={want[~same][:3]}"
+
+
 def test_device_sqrt_edges(gpu_tracer):
     """vm_sqrt's unwrapped fast path covers [2^-767, DBL_MAX]; everything else (and the range
     ends) must give sqrt()'s bits too: zeros, subnormals, the 2^-767 boundary, inf, NaN,
