@@ -573,6 +573,8 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         Q.sh_br = log2_exact(K.band_rows);
         Q.sh_bs = log2_exact(K.band_stride);
         Q.sh_c = log2_exact(Q.lay.C);
+        Q.rw = log2_exact(K.w) >= 0 ? 1.0 / K.w : 0.0;
+        Q.rh = log2_exact(K.h) >= 0 ? 1.0 / K.h : 0.0;
         const uint64_t units = (uint64_t)K.tiles_x * (uint64_t)K.tiles_y * 64u * (uint64_t)Q.nch;
         if (units >= 0xFFFFFFFFull) return vpt_fail(VPT_E_INVALID, "too many work units (%llu)", (unsigned long long)units);
         Q.seed = K.seed;

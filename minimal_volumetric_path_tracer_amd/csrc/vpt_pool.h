@@ -149,6 +149,7 @@ struct PoolParams {
      * two, else -1: the unit decode and the partial's address divide by them (a u32 division is ~15
      * VALU instructions; every lane of a wave runs it when one lane takes or finishes a unit) */
     int sh_lu, sh_tx, sh_br, sh_bs, sh_c;
+    double rw, rh;          /* 1/w, 1/h when w, h are powers of two (then u / w == u * rw exactly), else 0 */
     double* partials;       /* nch * rows * w * 3: chunk-major, so the units of one chunk level (handed
                              * out together, 8x8 tiles) write neighbouring 24-B records that merge into
                              * whole lines in L2 (pixel-major wrote 24 B per 128-B line: 2x the WRITE_SIZE) */
@@ -188,7 +189,11 @@ __device__ __forceinline__ dv3 pool_camera_dir(const PoolParams& P, double jx, d
 {
     const dv3 cd = mk(P.d[0], P.d[1], P.d[2]);
     const dv3 cx = mk(P.cx[0], P.cx[1], P.cx[2]), cy = mk(P.cy[0], P.cy[1], P.cy[2]);
-    dv3 dir = add(add(scl(cx, (((double)x + jx - 0.5) / P.w - .5)), scl(cy, (((double)y + jy - 0.5) / P.h - .5))), cd);
+    const double ux = (double)x + jx - 0.5, uy = (double)y + jy - 0.5;
+    /* division by a power of two is exact, as is the multiplication by its reciprocal (the operands
+     * are far from the subnormal range): the same bits without the division sequences */
+    const double fx = P.rw != 0 ? ux * P.rw : ux / P.w, fy = P.rh != 0 ? uy * P.rh : uy / P.h;
+    dv3 dir = add(add(scl(cx, (fx - .5)), scl(cy, (fy - .5))), cd);
     return nrm(dir);
 }
 
