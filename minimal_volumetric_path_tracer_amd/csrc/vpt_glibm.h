@@ -150,8 +150,11 @@ VM_QUAL double gm_cos(double x) { return gm_sc(vm_tab(gm_sc_tab), x, 1); }
  * entry sets are read unconditionally (same cache lines; re-reading them only when some lane of
  * the wave needed it, behind a ballot, was 21 % slower on the pool kernel: A/B 58.6 vs 70.9 ms).
  * FF 1024^2 x 256: 61.9 ms with two gm_sc calls -> 58.6 ms. */
-VM_QUAL void gm_sincos_fused(vm_ct* K, double x, double* sn_out, double* cs_out)
+VM_QUAL void gm_sincos_fused_r(vm_ct* K, double x, double* sn_out, double* cs_out, const int small, const int taylor)
 {
+    /* small: every lane of the wave has |x| < 0.855469 (glibc's first range: no reduction, no swap);
+     * taylor: and |x| < 0.126 (sin by TAYLOR_SIN, the do_sin table form unused).  Constant arguments
+     * at the call sites below, so each specialisation drops the work the range makes dead. */
     const uint32_t kx = (uint32_t)gm_hi(x) & 0x7fffffffu;
     const double ax = vm_fabs(x);
     /* reduce_sincos, as in gm_sc */
@@ -166,7 +169,7 @@ VM_QUAL void gm_sincos_fused(vm_ct* K, double x, double* sn_out, double* cs_out)
     const double hp1 = VM_T(K, GS_HP1);
     const double h = VM_T(K, GS_HP0) - ax;
     const double hs = h + hp1;
-    const int r2 = kx < 0x3feb6000u, r3 = kx < 0x400368fdu;
+    const int r2 = small ? 1 : kx < 0x3feb6000u, r3 = kx < 0x400368fdu;
     /* operands of the do_sin/Taylor evaluation (S) and of the do_cos evaluation (C) */
     const double aS = r2 ? x : r3 ? hs : b;
     const double daS = r2 ? 0.0 : r3 ? (h - hs) + hp1 : db;
@@ -205,7 +208,7 @@ VM_QUAL void gm_sincos_fused(vm_ct* K, double x, double* sn_out, double* cs_out)
     p = gm_fma(p, xx0, VM_T(K, GS_S5 + 3));
     p = gm_fma(p, xx0, VM_T(K, GS_S5 + 4));
     const double vT = gm_fma(xx0, fma(p, aS, -(0.5 * daS)), daS) + aS;
-    const double vSin = aaS < VM_T(K, GS_TAYLOR) ? vT : vS;
+    const double vSin = (taylor || aaS < VM_T(K, GS_TAYLOR)) ? vT : vS;
     /* do_cos: s = x + x xx P, cs + (((ccs - s ssn) - cs c) - sn s) */
     const double xxC = xC * xC;
     const double psC = gm_fma(VM_T(K, GS_SN5), xxC, VM_T(K, GS_SN3));
@@ -224,8 +227,14 @@ VM_QUAL void gm_sincos_fused(vm_ct* K, double x, double* sn_out, double* cs_out)
     s = kx < 0x3e500000u ? x : s;
     c = kx < 0x3e400000u ? 1.0 : c;
     const double nan = x - x + __builtin_nan("");
-    *sn_out = kx >= 0x419921fbu ? nan : s;
-    *cs_out = kx >= 0x419921fbu ? nan : c;
+    *sn_out = (!small && kx >= 0x419921fbu) ? nan : s;
+    *cs_out = (!small && kx >= 0x419921fbu) ? nan : c;
+}
+
+/* gm_sincos_fused_r for any x */
+VM_QUAL void gm_sincos_fused(vm_ct* K, double x, double* sn_out, double* cs_out)
+{
+    gm_sincos_fused_r(K, x, sn_out, cs_out, 0, 0);
 }
 
 /* ------------------------------------------------------------------ acos (e_asin.c) */
@@ -512,6 +521,18 @@ GM_CALLQ gm_sc2 gm_sincos2(double x0, double x1) { return gm_sincos2_inl(x0, x1)
 GM_CALLQ gm_sc2 gm_sincos_acos_phi(double c, double phi)
 {
     return gm_sincos2_inl(gm_acos(c), phi);
+}
+
+/* gm_sincos_acos_phi for a wave whose every c > 0.9925 (the cone toward a sphere light): acos(c) <
+ * 0.1226 < 0.126 in every lane (glibc's acos is within an ulp), so sin of the polar angle is
+ * TAYLOR_SIN and cos its first-range do_cos -- the specialised evaluation, the same bits */
+GM_CALLQ gm_sc2 gm_sincos_acos_phi_cone(double c, double phi)
+{
+    vm_ct* K = vm_tab(gm_sc_tab);
+    gm_sc2 r;
+    gm_sincos_fused_r(K, gm_acos(c), &r.s0, &r.c0, 1, 1);
+    gm_sincos_k(K, phi, &r.s1, &r.c1);
+    return r;
 }
 
 /* sin(x), cos(x) */
