@@ -414,9 +414,9 @@ VM_QUAL double gm_log(double x)
  * glibc 2.35's __ieee754_atan2, FMA build, for x > 0: atan(|y|/x) (|y| < x) or pi/2 - atan(x/|y|)
  * (x <= |y|) from u = min/max and its correction du, by an odd polynomial (u < 1/16) or around a
  * node of the cij table (7 doubles per node), sign of y.  The four forms are evaluated branch-free
- * and selected.  Everything else -- x <= 0, y = 0, NaN, inf, |y|/x far outside [2^-57, 2^57] (the
- * exponent-difference shortcuts), operands the library rescales (below 2^-500 or above 2^500) --
- * goes to the translated gl_atan2.  The equi-angular setup (include/volumetricBasicFunctions.h:
+ * and selected; |y|/x above 2^57 gives +-hpi.  Everything else -- x <= 0, y = 0, NaN, inf, |y|/x
+ * below 2^-57, operands the library rescales (below 2^-500 or above 2^500) -- goes to the
+ * translated gl_atan2.  The equi-angular setup (include/volumetricBasicFunctions.h:
  * 209-223) calls atan2(-proj, D) and atan2(tMax - proj, D) with D > 0. */
 VM_TABLE(gm_atan2_tab, {
     0x1.375f08b31cbcep-4, -0x1.7458022b13c25p-4, 0x1.c71c6e5129a3bp-4, -0x1.24924923f7603p-3,
@@ -466,10 +466,13 @@ VM_QUAL double gm_atan2(double y, double x)
     const double z_ii_tab = (hpi - c1) + gm_fnma(w2, q2, hpi1);
     const int small = u < 0.0625;
     const double z = ci ? (small ? z_i_poly : z_i_tab) : (small ? z_ii_poly : z_ii_tab);
-    double r = vm_copysign(z, y);
+    /* |y| / x above 2^57 (exponent difference; tMax = MAXFLOAT of a ray that leaves the scene):
+     * atan2 = pi/2 - (less than 2^-57), whose correctly rounded value -- glibc's result there -- is
+     * the double hpi (pi/2 - hpi = 6.1e-17 < half an ulp), with y's sign */
+    double r = vm_copysign(de > 0x38fffff ? hpi : z, y);
     const double tm500 = VM_T(K, GT_TM500), t500 = VM_T(K, GT_T500);
     const int rare = !(x > 0.0) || !(ay > 0.0) || !(x < __builtin_inf()) || !(ay < __builtin_inf()) ||
-                     de > 0x38fffff || de < -0x38fffff || ax < tm500 || ay < tm500 || ax > t500 || ay > t500;
+                     de < -0x38fffff || ax < tm500 || ay < tm500 || ax > t500 || ay > t500;
     if (rare) r = gl_atan2(y, x);
     return r;
 }

@@ -55,6 +55,19 @@ def test_device_sqrt_div_correctly_rounded(gpu_tracer, orc):
     assert bitwise_equal(gpu_tracer.math_probe(9, x, y), x / y).all()
 
 
+def test_device_atan2_huge_ratio(gpu_tracer, orc):
+    """gm_atan2's |y|/x > 2^57 shortcut (+-hpi; the equi-angular atan2(MAXFLOAT - proj, D) of an
+    escaping ray) == glibc's atan2 on the device too"""
+    rng = np.random.default_rng(13)
+    x = np.exp(rng.uniform(-30, 30, 100000))
+    y = x * 2.0 ** rng.uniform(50, 75, 100000) * rng.choice([-1.0, 1.0], 100000)
+    D = np.exp(rng.uniform(-8, 7, 4000))
+    ym = np.float64(3.4028234663852886e38) - rng.uniform(-400, 400, 4000)
+    y, x = np.concatenate([y, ym, -ym]), np.concatenate([x, D, D])
+    got, want = gpu_tracer.math_probe(8, y, x), orc.math(8, y, x)
+    assert bitwise_equal(got, want).all()
+
+
 def test_device_inv_sqrt_exact(gpu_tracer):
     """vm_inv_sqrt (nrm's 1.0 / sqrt(|a|^2): the square root and the division sequences without their
     scaling / fix-up steps inside [2^-767, DBL_MAX]) == 1.0 / np.sqrt(x) bit for bit, across the
