@@ -189,7 +189,9 @@ def cpu_baseline(img: np.ndarray, c: dict, threads: int) -> dict:
     tls, asis = os.path.join(ROOT, "oracle", "_ref", "rt_tls"), os.path.join(ROOT, "oracle", "_ref", "rt")
     px = 1024 * 768
     spp_n, spp_1, spp_a = 64, 4, 16
-    el_n = run_reference_program(tls, spp_n, cpus)
+    # best of two: the box's other tenants can slow one 2-3 s run by 10-20 % (the socket estimate and
+    # the north-star ratio scale with this number)
+    el_n = min(run_reference_program(tls, spp_n, cpus), run_reference_program(tls, spp_n, cpus))
     el_1 = run_reference_program(tls, spp_1, cpus[:1])
     el_a = run_reference_program(asis, spp_a, cpus)
     v_n, v_1, v_a = px * spp_n / el_n / 1e6, px * spp_1 / el_1 / 1e6, px * spp_a / el_a / 1e6
@@ -198,7 +200,7 @@ def cpu_baseline(img: np.ndarray, c: dict, threads: int) -> dict:
         "value": v_n, "unit": "Msamples/s", "cores": len(cpus), "kind": "reference",
         "sample": f"reference program src/rt.cpp with a per-thread erand48 state (oracle/_ref/rt_tls), "
                   f"`rt_tls {spp_n}` = 1024x768x{spp_n} free-flight, default scene, {len(cpus)} OpenMP threads "
-                  f"pinned to {len(cpus)} physical cores of socket 0, elapsed {el_n:.2f}s incl. its PPM write",
+                  f"pinned to {len(cpus)} physical cores of socket 0, elapsed {el_n:.2f}s incl. its PPM write (best of 2 runs)",
         "cpu_model": topo["model"],
         "socket_physical_cores": S,
         "one_core": {"value": v_1, "sample": f"rt_tls {spp_1}, 1 thread, {el_1:.2f}s"},
