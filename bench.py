@@ -68,7 +68,8 @@ CONFIGS = {
 }
 
 
-def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 12, band: int = 16) -> dict:
+def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 12, band: int = 16, ref_rate=None,
+                   cal_spp: int = 16) -> dict:
     """The oracle restatement (oracle/liboracle_vm.so: per-sample streams, the kernel's portable
     libm) timed on `bands` bands of `band` camera rows of the bench image, same seed and chunk
     layout, and compared with the GPU image on those rows: per-channel RMSE of the linear float32
@@ -81,6 +82,13 @@ def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 12, band
     from minimal_volumetric_path_tracer_amd.tracer import ESTIMATORS
 
     est = ESTIMATORS[c["estimator"]]
+    # pinned like the reference program (its OpenMP threads inherit this mask when first created)
+    saved = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, cpu_topology(threads)["cpus"])
+    # calibration on the reference program's own workload (1024 x 768 free flight, all rows)
+    t = time.time()
+    o.render(1024, 768, cal_spp, 0, seed=0x5EED0001, threads=threads)
+    cal = 1024 * 768 * cal_spp / (time.time() - t) / 1e6
     se, n, el = np.zeros(3), 0, 0.0
     for k in range(bands):
         y0 = (H - band) * k // max(bands - 1, 1)
@@ -92,10 +100,16 @@ def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 12, band
         d = img[rows].astype(np.float64) - ref[rows].astype(np.float32).astype(np.float64)
         se += (d * d).reshape(-1, 3).sum(0)
         n += band * W
-    return {"value": bands * band * W * SPP / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle restatement (per-sample erand48 streams, portable libm), {bands} bands of {band} rows "
-                      f"x {W} x {SPP} spp of the bench image, {threads} threads, {el:.1f}s",
-            "rmse_vs_gpu_per_channel": [float(x) for x in np.sqrt(se / n)]}
+    os.sched_setaffinity(0, saved)
+    res = {"value": bands * band * W * SPP / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": f"oracle restatement (per-sample erand48 streams, the device's math layer), {bands} bands of "
+                     f"{band} rows x {W} x {SPP} spp of the bench image, {threads} threads pinned as the reference, "
+                     f"{el:.1f}s",
+           "rmse_vs_gpu_per_channel": [float(x) for x in np.sqrt(se / n)],
+           "calibration": {"value": cal, "workload": f"1024x768x{cal_spp} free flight, all rows, {threads} threads"}}
+    if ref_rate:
+        res["calibration"]["vs_reference_program"] = round(cal / ref_rate, 3)
+    return res
 
 
 def cpu_topology(threads: int) -> dict:
@@ -443,7 +457,8 @@ def main() -> None:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         if world == 1 and not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(img, c, threads)
-            res["cpu_baseline"]["port_per_sample_rng"] = cpu_port_check(img, c, threads, bands=4)
+            res["cpu_baseline"]["port_per_sample_rng"] = cpu_port_check(img, c, threads, bands=4,
+                                                                         ref_rate=res["cpu_baseline"]["value"])
             cb0 = res["cpu_baseline"]
             # ratios of this line's value to the reference program (vs_baseline stays null: BASELINE.md
             # holds no published number for this metric)

@@ -21,10 +21,10 @@ def test_cpu_port_check_rmse():
     o = Oracle(portable=True)
     o.set_scene(vpt.default_scene())
     img = o.render(48, 32, 3, 0, seed=0x5EED0001, threads=2).astype(np.float32)
-    r = bench.cpu_port_check(img, c, threads=2, bands=2, band=16)
+    r = bench.cpu_port_check(img, c, threads=2, bands=2, band=16, cal_spp=1)
     assert r["kind"] == "port" and r["rmse_vs_gpu_per_channel"] == [0.0, 0.0, 0.0] and r["value"] > 0
     img[0, 5, 1] += 0.5  # file row 0 = camera row 31, inside the top band
-    assert bench.cpu_port_check(img, c, threads=2, bands=2, band=16)["rmse_vs_gpu_per_channel"][1] > 0
+    assert bench.cpu_port_check(img, c, threads=2, bands=2, band=16, cal_spp=1)["rmse_vs_gpu_per_channel"][1] > 0
 
 
 def test_bench_configs_match_baseline():
