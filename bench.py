@@ -70,14 +70,15 @@ CONFIGS = {
 
 def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 12, band: int = 16, ref_rate=None,
                    cal_spp: int = 16) -> dict:
-    """The oracle restatement (oracle/liboracle_vm.so: per-sample streams, the kernel's portable
-    libm) timed on `bands` bands of `band` camera rows of the bench image, same seed and chunk
-    layout, and compared with the GPU image on those rows: per-channel RMSE of the linear float32
+    """The oracle restatement (oracle/liboracle.so: per-sample streams, glibc's libm called directly
+    like the reference; built with the reference program's -O3 -march=x86-64-v3, contraction off)
+    timed on `bands` bands of `band` camera rows of the bench image, same seed and chunk layout,
+    and compared with the GPU image on those rows: per-channel RMSE of the linear float32
     framebuffer (the metric's "per-channel RMSE vs CPU"; the bar is bit-exact, RMSE 0)."""
     from oracle.oracle import Oracle  # cpu_baseline leg only
 
     H, W, SPP = c["height"], c["width"], c["spp"]
-    o = Oracle(portable=True)
+    o = Oracle(portable=False)
     o.set_scene(vpt.default_scene())
     from minimal_volumetric_path_tracer_amd.tracer import ESTIMATORS
 
@@ -102,7 +103,7 @@ def cpu_port_check(img: np.ndarray, c: dict, threads: int, bands: int = 12, band
         n += band * W
     os.sched_setaffinity(0, saved)
     res = {"value": bands * band * W * SPP / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-           "sample": f"oracle restatement (per-sample erand48 streams, the device's math layer), {bands} bands of "
+           "sample": f"oracle restatement (per-sample erand48 streams, glibc libm), {bands} bands of "
                      f"{band} rows x {W} x {SPP} spp of the bench image, {threads} threads pinned as the reference, "
                      f"{el:.1f}s",
            "rmse_vs_gpu_per_channel": [float(x) for x in np.sqrt(se / n)],
