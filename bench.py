@@ -221,8 +221,9 @@ def cpu_baseline(img: np.ndarray, c: dict, threads: int) -> dict:
         "one_core": {"value": v_1, "sample": f"rt_tls {spp_1}, 1 thread, {el_1:.2f}s"},
         "parallel_efficiency": v_n / (v_1 * len(cpus)),
         "socket_estimate": {"value": v_n * S / len(cpus),
-                            "how": f"measured {len(cpus)}-core rate x {S}/{len(cpus)} (the per-thread flavour has no "
-                                   f"shared state; the job's CPU share is {len(cpus)} cores, not the socket)"},
+                            "how": f"EXTRAPOLATION, not a measurement: measured {len(cpus)}-core rate x {S}/{len(cpus)} "
+                                   f"(the per-thread flavour has no shared state; the job's CPU share is {len(cpus)} "
+                                   f"cores, not the socket, so the other {S - len(cpus)} cores cannot be run)"},
         "as_written": {"value": v_a, "kind": "reference",
                        "sample": f"oracle/_ref/rt (src/rt.cpp unchanged: one erand48 state shared by all threads, "
                                  f"SURVEY H4), `rt {spp_a}`, {len(cpus)} threads on the same cores, {el_a:.2f}s"},
@@ -454,6 +455,7 @@ def main() -> None:
                         "(committed PMC profile of this command, profiles/r*/pmc_pool_kernel.json)",
             },
             "image_mean": [round(float(x), 6) for x in img.reshape(-1, 3).mean(0)],
+            "build_id": vpt.build_id(),
         }
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         if world == 1 and not args.no_cpu:
@@ -490,7 +492,11 @@ def main() -> None:
                 o["cpu_reference"] = {"one_core": mis1, "socket_estimate": sock,
                                       "how": "reference MISVPTTracerRecursive (oracle/_ref/libvpt_ref.so), 2 rows x "
                                              f"{cn['width']} x 32 spp on one core, x parallel efficiency "
-                                             f"{cb['parallel_efficiency']:.2f} x {cb['socket_physical_cores']} cores"}
+                                             f"{cb['parallel_efficiency']:.2f} x {cb['socket_physical_cores']} cores "
+                                             "(an extrapolation from one core: the job has 16 cores, not the socket)",
+                                      "phase": "the CPU side runs the reference's ISOTROPIC phase (it has no HG); the "
+                                               "GPU side runs HG g=0.5 (the north-star extension, g=0 reduces to "
+                                               "the reference bit for bit)"}
                 o["speedup_vs_cpu_socket"] = round(ns["value"] / sock, 1)
                 o["target_speedup"] = 100
             res["north_star"] = o

@@ -206,6 +206,15 @@ uint64_t vpt_stream_state(uint64_t seed, uint64_t pixel_idx, uint64_t sample);
  * normalisation's reciprocal).  Host arrays, synchronous (parity tests). */
 int vpt_math_probe(vpt_context* ctx, int fn, const double* x, const double* y, double* out, int n);
 
+/* Henyey-Greenstein phase extension (the north-star's HG g; the reference has only the isotropic
+ * phase, include/vptSamplingFunctions.h:34-47 and include/volumetricBasicFunctions.h:59-62, which
+ * g == 0 reproduces bit for bit).  For each of the n erand48 states: the direction the medium event
+ * samples around the propagation direction din (two draws), and the state after them; for each of
+ * the nw directions wl: the phase value the NEE weights with (mu = din . wl).  Host arrays,
+ * synchronous (property tests). */
+int vpt_phase_probe(vpt_context* ctx, double g, const double din[3], const uint64_t* states, int n, double* dirs,
+                    uint64_t* states_out, const double* wl, int nw, double* values);
+
 /* PPM writer of main() (src/rt.cpp:812-820): clamp to [0,1] (src/rt.cpp:803), gamma 1/2.2,
  * int(v*255 + .5) (include/mathUtilities.h:43-45), "P3\n%d %d\n255\n" then "%d %d %d " per
  * pixel, byte-identical.  rgb: host framebuffer, w*h*3 of fb_format, file order. */
@@ -215,6 +224,9 @@ int64_t vpt_encode_ppm(const void* rgb, int fb_format, int w, int h, char* buf, 
 
 const char* vpt_last_error(void);
 int vpt_abi_version(void);
+/* Build provenance: 16 hex digits hashing the library's sources and compile flags
+ * (scripts/build_id.py, baked in by csrc/Makefile). */
+const char* vpt_build_id(void);
 
 #ifdef __cplusplus
 }

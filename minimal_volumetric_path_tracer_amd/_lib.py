@@ -100,10 +100,13 @@ PROTOTYPES = [
     ("vpt_count_work", c_int, [c_void_p, POINTER(vpt_params), POINTER(c_uint64), POINTER(c_uint64)]),
     ("vpt_stream_state", c_uint64, [c_uint64, c_uint64, c_uint64]),
     ("vpt_math_probe", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int]),
+    ("vpt_phase_probe", c_int, [c_void_p, c_double, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                c_void_p]),
     ("vpt_write_ppm", c_int, [c_char_p, c_void_p, c_int, c_int, c_int]),
     ("vpt_encode_ppm", c_int64, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64]),
     ("vpt_last_error", c_char_p, []),
     ("vpt_abi_version", c_int, []),
+    ("vpt_build_id", c_char_p, []),
 ]
 
 
@@ -123,6 +126,11 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def build_id() -> str:
+    """The loaded library's build id (sources + flags hash, scripts/build_id.py)."""
+    return lib().vpt_build_id().decode()
 
 
 def check(rc: int) -> None:

@@ -38,6 +38,9 @@
 #ifndef VPT_FUSE_RAYS
 #define VPT_FUSE_RAYS 3
 #endif
+#ifndef VPT_FUSE_RARE_MONO
+#define VPT_FUSE_RARE_MONO 0  /* 1: the fused MISv2 only for diffuse surfaces (MK == 0) */
+#endif
 /* sphere loops taken G spheres at a time (scene_intersect_grouped): decide() and every other
  * site; A/B at 1024^2 x 256: off 4914, decide only G=5 4967 (G=10 4857), all sites G=5 5042, G=3 5009 */
 #ifndef VPT_DECIDE_GROUP
@@ -63,6 +66,69 @@ namespace vpt {
 #else
 #define ISECT_SQRT(x) vm_sqrt(x)
 #endif
+
+/* Debug section timers (builds with -DVPT_SECTIONS=1 only; scripts/sect_stats.py): the wave's
+ * s_memtime cycles spent in each section, accumulated per
+ * wave in LDS by its first active lane and flushed to g_vpt_sect[k] (entries: g_vpt_sect[SECT_N + k])
+ * when the wave exits (sect_flush).  Wall cycles of one wave: the co-resident waves' issue shares
+ * the SIMD, so these are shares of time, not instruction counts. */
+#ifndef VPT_SECTIONS
+#define VPT_SECTIONS 0
+#endif
+enum {
+    SECT_SCHED = 0, SECT_LOAD, SECT_S_PLIGHT, SECT_S_MIS, SECT_S_MIS_ISECT, SECT_S_BDSF, SECT_M_SS, SECT_M_SS_DIR,
+    SECT_M_SS_ISECT, SECT_M_SS_SHADOW, SECT_M_PHASE, SECT_CONT, SECT_A_PREP, SECT_A_DECIDE, SECT_A_ISECT, SECT_STORE,
+    SECT_S_TOTAL, SECT_M_TOTAL, SECT_A_CAMERA, SECT_USED, SECT_N = 32
+};
+#if VPT_SECTIONS
+__device__ unsigned long long g_vpt_sect[2 * SECT_N];
+__device__ static inline __attribute__((always_inline)) uint32_t* sect_lds()
+{
+    __shared__ uint32_t a[16][2 * SECT_USED];  /* per wave: cycles, entries */
+    return &a[(threadIdx.x >> 6) & 15][0];
+}
+#endif
+__device__ static inline __attribute__((always_inline)) uint32_t sect_now()
+{
+#if VPT_SECTIONS
+    return (uint32_t)__builtin_amdgcn_s_memtime();  /* (gfx950 reads HW_REG_SHADER_CYCLES as 0) */
+#else
+    return 0;
+#endif
+}
+__device__ static inline __attribute__((always_inline)) void sect_add(int k, uint32_t t0)
+{
+#if VPT_SECTIONS
+    const uint32_t dt = sect_now() - t0;
+    const int first = __ffsll((unsigned long long)__ballot(1)) - 1;
+    if ((int)(threadIdx.x & 63) == first) {
+        uint32_t* a = sect_lds();
+        a[k] += dt;
+        a[SECT_USED + k] += 1;
+    }
+#else
+    (void)k;
+    (void)t0;
+#endif
+}
+__device__ static inline __attribute__((always_inline)) void sect_init()
+{
+#if VPT_SECTIONS
+    if ((threadIdx.x & 63) < 2 * SECT_USED) sect_lds()[threadIdx.x & 63] = 0;
+#endif
+}
+__device__ static inline __attribute__((always_inline)) void sect_flush()
+{
+#if VPT_SECTIONS
+    const int l = threadIdx.x & 63;
+    if (l < 2 * SECT_USED) {
+        const uint32_t v = sect_lds()[l];
+        atomicAdd(&g_vpt_sect[l < SECT_USED ? l : SECT_N + l - SECT_USED], (unsigned long long)v);
+    }
+#endif
+}
+#define SECT_BEGIN(name) const uint32_t _sect_##name = sect_now()
+#define SECT_END(name, k) sect_add(k, _sect_##name)
 
 /* ------------------------------------------------------------------ vectors (Vector.h:10-36) */
 struct dv3 {
@@ -224,10 +290,49 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
 #ifndef VPT_ISECT_GROUP_ALL
 #define VPT_ISECT_GROUP_ALL 5
 #endif
+/* intersect() out of line (VPT_ISECT_CALL): one copy of the sphere loop serves every site instead of
+ * ~3 KB of unrolled loop per site -- the kernel's hot code, not its arithmetic, is what a smaller
+ * copy count buys (the instruction cache is shared by two CUs).  The callee's registers are the
+ * caller-saved ones, so the caller keeps its live values in place across the call. */
+#ifndef VPT_ISECT_CALL
+#define VPT_ISECT_CALL 0  /* A/B: FF 55.29 -> 56.11 ms, MIS 257.8 -> 277.2 (with VPT_ONE_A) */
+#endif
+struct IsectR {
+    double t;
+    int id, hit;
+};
+__device__ static __attribute__((noinline)) IsectR isect_ool(const DevScene* __restrict__ S, dv3 o, dv3 d, int id0)
+{
+    /* the scene pointer is wave-uniform: back to SGPRs, so that the sphere records come through
+     * scalar loads as in the inlined loop */
+    const uint64_t pv = (uint64_t)S;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pv >> 32));
+    const DevScene* __restrict__ Su = (const DevScene*)(((uint64_t)hi << 32) | lo);
+    Sampler<false> smp;
+    IsectR r;
+    r.id = id0;
+#if VPT_ISECT_GROUP_ALL > 1
+    r.hit = scene_intersect_grouped<VPT_ISECT_GROUP_ALL>(Su, smp, o, d, r.t, r.id);
+#else
+    r.hit = scene_intersect(Su, smp, o, d, r.t, r.id, false);
+#endif
+    return r;
+}
+
 template <bool COUNT>
 VPT_DEV int scene_isect(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, double& t, int& id,
                         bool skip3)
 {
+#if VPT_ISECT_CALL && defined(__HIP_DEVICE_COMPILE__)
+    if (!skip3) {
+        const IsectR r = isect_ool(S, o, d, id);
+        smp.tests(S->n);
+        t = r.t;
+        id = r.id;
+        return r.hit;
+    }
+#endif
 #if VPT_ISECT_GROUP_ALL > 1
     if (!skip3) return scene_intersect_grouped<VPT_ISECT_GROUP_ALL>(S, smp, o, d, t, id);
 #endif
@@ -463,8 +568,18 @@ VPT_DEV double microfacet_prob(dv3 wo, dv3 wh, double alpha, dv3 n)
     return ndf(dot(wh, n), alpha) * num / den;
 }
 
-/* frMicroFacet, :95-100 (G_smith :63-68) */
-VPT_DEV dv3 fr_microfacet(dv3 eta, dv3 kappa, dv3 wi, dv3 wh, dv3 wo, double alpha, dv3 n)
+/* frMicroFacet, :95-100 (G_smith :63-68).  Out of line on the device (VPT_FR_CALL): three Fresnel
+ * channels, two Smith terms and the NDF are independent chains that the scheduler interleaves, and
+ * inlined at the five sites of a metal surface event they set the kernel's register allocation. */
+#ifndef VPT_FR_CALL
+#define VPT_FR_CALL 0       /* A/B (with VPT_FUSE_RARE_MONO): 53.28 vs 53.50 ms FF, 263.5 vs 260.9 MIS */
+#endif
+#if VPT_FR_CALL
+#define VPT_FR_QUAL __device__ static __attribute__((noinline))
+#else
+#define VPT_FR_QUAL VPT_DEV
+#endif
+VPT_FR_QUAL dv3 fr_microfacet(dv3 eta, dv3 kappa, dv3 wi, dv3 wh, dv3 wo, double alpha, dv3 n)
 {
     double den = (4 * vm_fabs(dot(n, wi)) * vm_fabs(dot(n, wo)));
     double G = g1(n, wi, wh, alpha) * g1(n, wo, wh, alpha);
@@ -755,7 +870,9 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     int ids[3] = {0, 0, 0};
     bool hits[3];
 #if VPT_FUSE_RAYS == 3
+    SECT_BEGIN(mi);
     scene_intersect_n<3>(S, smp, x, dirs, tt, ids, hits);
+    SECT_END(mi, SECT_S_MIS_ISECT);
 #else
     {
         const dv3 d2[2] = {dirs[0], dirs[1]};
@@ -929,6 +1046,7 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     const dv3 rad = sph_rad(S, src);
     const bool point = LT == 1 || (LT < 0 && lr == 0);
     dv3 Ld = mk(0, 0, 0);
+    SECT_BEGIN(sd);
     dv3 wc = sub(lp, xt);
     double mag = vm_sqrt(dot(wc, wc));
     wc = scl(wc, (1 / mag));
@@ -937,9 +1055,13 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     double cmax = LT == 1 ? (mag > 0 ? 1.0 : __builtin_nan("")) : vm_sqrt(1 - lr / mag * (lr / mag));
     dv3 wl = solid_angle_dir(smp, wc, cmax);
     double prob_wl = solid_angle_prob(cmax);
+    SECT_END(sd, SECT_M_SS_DIR);
+    SECT_BEGIN(si);
     double tdist;
     int idHit = 0;
     scene_isect(S, smp, xt, wl, tdist, idHit, false);
+    SECT_END(si, SECT_M_SS_ISECT);
+    SECT_BEGIN(sw);
     if (src == idHit) {
         if (point) smp.tests(S->n);  /* the shadow ray the reference casts first (result overwritten) */
         double it = lm_exp(sigma_t * tdist * -1.0);
@@ -957,6 +1079,7 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
             else Ld = scl(Ls, (1 / probSource));
         }
     }
+    SECT_END(sw, SECT_M_SS_SHADOW);
     return Ld;
 }
 
@@ -1040,11 +1163,15 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
     const double sigma_t = m.sigma_a + m.sigma_s;
     int id = 0;
     double t;
-#if VPT_DECIDE_GROUP > 1
+    SECT_BEGIN(di);
+#if VPT_ISECT_CALL && defined(__HIP_DEVICE_COMPILE__)
+    const bool hit = scene_isect(S, smp, p.o, p.d, t, id, false);
+#elif VPT_DECIDE_GROUP > 1
     const bool hit = scene_intersect_grouped<VPT_DECIDE_GROUP>(S, smp, p.o, p.d, t, id);
 #else
     const bool hit = scene_intersect(S, smp, p.o, p.d, t, id, false);
 #endif
+    SECT_END(di, SECT_A_ISECT);
     if constexpr (EST == 5) {  /* iterativePathTracer (shadeMethods.h:115-125): nearest hit or end */
         if (COUNT) smp.cnt.iterations++;
         e.t = t;
@@ -1120,14 +1247,20 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     }
     const double probSource = 1.0 / S->n_emit;
     const double alpha = S->sph[id].alpha;
+    SECT_BEGIN(pl);
     double Trs = transmitance(xs, sph_p(S, src), sigma_t);
     dv3 Ldp = scl(scl(p_light<COUNT, MK, PT>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+    SECT_END(pl, SECT_S_PLIGHT);
+    SECT_BEGIN(mis);
 #if VPT_FUSE_RAYS
-    dv3 Ld = S->n_mis == 2 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
-                           : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
+    dv3 Ld = (MK == 0 || !VPT_FUSE_RARE_MONO) && S->n_mis == 2
+                 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
+                 : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
 #else
     dv3 Ld = mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
 #endif
+    SECT_END(mis, SECT_S_MIS);
+    SECT_BEGIN(bd);
     dv3 wi = mk(0, 0, 0);
     double pdf = 0;
     dv3 fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
@@ -1139,6 +1272,7 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     p.o = xs;
     p.d = wi;
     p.depth++;
+    SECT_END(bd, SECT_S_BDSF);
 }
 
 /* medium event: single-scattering NEE toward the picked light, phase-function continuation.
@@ -1196,8 +1330,12 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
     }
     const double probSource = 1.0 / S->n_emit;
     if (EST == 0) {
+        SECT_BEGIN(ss);
         dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
+        SECT_END(ss, SECT_M_SS);
+        SECT_BEGIN(ph);
         dv3 wi = phase_sample(smp, p.d);
+        SECT_END(ph, SECT_M_PHASE);
         p.L = add(p.L, scl(scl(mul(Ld, p.beta), (sigma_s / sigma_t)), (1 / continueprob)));
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
@@ -1209,8 +1347,12 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
         p.d = wi;
     } else {
         double T = transmitance(p.o, xt, sigma_t);
+        SECT_BEGIN(ss);
         dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, true, sigma_s, T, probSource);
+        SECT_END(ss, SECT_M_SS);
+        SECT_BEGIN(ph);
         dv3 wi = phase_sample(smp, p.d);
+        SECT_END(ph, SECT_M_PHASE);
         p.L = add(p.L, mul(p.beta, scl(scl(Ld, (1 / e.pdf)), (1 / continueprob))));
         p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / e.pdf));
         p.d = wi;

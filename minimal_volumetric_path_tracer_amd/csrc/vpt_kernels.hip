@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -342,6 +343,27 @@ __global__ void math_probe_kernel(int fn, const double* x, const double* y, doub
     out[i] = r;
 }
 
+/* HG extension probe: phase_sample around din from each state (the two draws of the stream), and
+ * phase_value toward each wl (vpt_phase_probe) */
+__global__ void phase_probe_kernel(double g, double dx, double dy, double dz, const uint64_t* X, int n, double* dirs,
+                                   uint64_t* Xout, const double* wl, int nw, double* vals)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const dv3 din = mk(dx, dy, dz);
+    if (i < n) {
+        Sampler<false> smp;
+        smp.X = X[i];
+        smp.g = g;
+        smp.cnt.tests = smp.cnt.iterations = 0;
+        const dv3 w = phase_sample(smp, din);
+        dirs[3 * i] = w.x;
+        dirs[3 * i + 1] = w.y;
+        dirs[3 * i + 2] = w.z;
+        Xout[i] = smp.X;
+    }
+    if (i < nw) vals[i] = phase_value(g, din, mk(wl[3 * i], wl[3 * i + 1], wl[3 * i + 2]));
+}
+
 bool is_finite(double v) { return v == v && v - v == 0.0; }
 
 unsigned long long* g_pool_stats = nullptr;  /* debug statistics buffer (VPT_POOL_STATS=1) */
@@ -357,7 +379,12 @@ struct StreamSlot {
     unsigned* d_queue;
     double* d_partials;      /* chunk sums of the pool kernel */
     size_t partials_bytes;
+    hipEvent_t done;         /* recorded after the slot's last launch */
+    unsigned long long used; /* last use (context tick), for reuse by another stream */
 };
+/* at most this many slots (each holds a partials buffer): a further stream takes over the least
+ * recently used slot whose work has finished, or waits for the least recently used one */
+constexpr int MAX_STREAM_SLOTS = 8;
 
 struct vpt_context {
     int device;
@@ -365,23 +392,42 @@ struct vpt_context {
     DevScene h_scene;
     int has_scene;
     unsigned long long* d_counters;
-    std::mutex mu;           /* guards slots */
-    std::vector<StreamSlot> slots;
+    std::mutex mu;           /* guards slots: held from taking a slot until its launches are enqueued */
+    std::vector<std::unique_ptr<StreamSlot>> slots;  /* stable addresses */
+    unsigned long long tick = 0;
 };
 
-/* the stream's slot, created on first use; partials grown to `pbytes` in stream order (the
- * previous buffer is freed after the work already queued on the stream) */
+/* The stream's slot, created on first use (or taken over from an idle stream once MAX_STREAM_SLOTS
+ * exist); partials grown to `pbytes` in stream order (the previous buffer is freed after the work
+ * already queued on the stream).  The caller holds ctx->mu from here until its launches on the slot
+ * are enqueued and slot_done() has recorded them, so no other thread can grow, free or hand over the
+ * slot's buffers in between. */
 static int stream_slot(vpt_context* ctx, hipStream_t stream, size_t pbytes, StreamSlot** out)
 {
-    std::lock_guard<std::mutex> lock(ctx->mu);
     StreamSlot* sl = nullptr;
     for (auto& x : ctx->slots)
-        if (x.stream == stream) sl = &x;
-    if (!sl) {
-        StreamSlot n{stream, nullptr, nullptr, 0};
-        HIP_OK(hipMalloc((void**)&n.d_queue, sizeof(unsigned)));
-        ctx->slots.push_back(n);
-        sl = &ctx->slots.back();
+        if (x->stream == stream) sl = x.get();
+    if (!sl && (int)ctx->slots.size() < MAX_STREAM_SLOTS) {
+        std::unique_ptr<StreamSlot> n(new StreamSlot{stream, nullptr, nullptr, 0, nullptr, 0});
+        HIP_OK(hipMalloc((void**)&n->d_queue, sizeof(unsigned)));
+        const hipError_t e = hipEventCreateWithFlags(&n->done, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            (void)hipFree(n->d_queue);
+            return vpt_fail(VPT_E_HIP, "hipEventCreateWithFlags: %s", hipGetErrorString(e));
+        }
+        ctx->slots.push_back(std::move(n));
+        sl = ctx->slots.back().get();
+    }
+    if (!sl) {  /* every slot belongs to another stream: take an idle one, else wait for the oldest */
+        StreamSlot* idle = nullptr;
+        StreamSlot* oldest = nullptr;
+        for (auto& x : ctx->slots) {
+            if (!oldest || x->used < oldest->used) oldest = x.get();
+            if (hipEventQuery(x->done) == hipSuccess && (!idle || x->used < idle->used)) idle = x.get();
+        }
+        sl = idle ? idle : oldest;
+        if (!idle) HIP_OK(hipEventSynchronize(sl->done));
+        sl->stream = stream;  /* its buffers are no longer read by the previous stream */
     }
     if (pbytes > sl->partials_bytes) {
         if (sl->d_partials) HIP_OK(hipFreeAsync(sl->d_partials, stream));
@@ -390,7 +436,15 @@ static int stream_slot(vpt_context* ctx, hipStream_t stream, size_t pbytes, Stre
         HIP_OK(hipMallocAsync((void**)&sl->d_partials, pbytes, stream));
         sl->partials_bytes = pbytes;
     }
+    sl->used = ++ctx->tick;
     *out = sl;
+    return VPT_OK;
+}
+
+/* after the slot's launches: its event marks when the stream is done with its buffers */
+static int slot_done(StreamSlot* sl, hipStream_t stream)
+{
+    HIP_OK(hipEventRecord(sl->done, stream));
     return VPT_OK;
 }
 
@@ -585,6 +639,7 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
             Q.cy[i] = K.cy[i];
         }
         const size_t pbytes = (size_t)K.shard_rows * (size_t)K.w * (size_t)Q.nch * 3 * sizeof(double);
+        std::lock_guard<std::mutex> lock(ctx->mu);  /* until the launches on the slot are enqueued */
         StreamSlot* sl = nullptr;
         rc = stream_slot(ctx, stream, pbytes, &sl);
         if (rc) return rc;
@@ -601,7 +656,11 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         /* The pool's ring positions are 32-bit counters that grow by ~3 per sample a workgroup
          * runs: launches are capped at 2^26 samples per workgroup (units in order, one partial
          * slot each, so splitting changes no value); one launch up to ~17 G samples on 256 CUs. */
-        const uint64_t max_units = (((uint64_t)1 << 26) * (uint64_t)blocks) / (uint64_t)(K.chunk > 0 ? K.chunk : 1);
+        /* (samples per unit: at most the layout's head chunk C; a unit above 2^26 samples is refused) */
+        if (Q.lay.C > (1 << 26))
+            return vpt_fail(VPT_E_INVALID, "chunk of %d samples > 2^26 (the per-workgroup launch bound)", Q.lay.C);
+        uint64_t max_units = (((uint64_t)1 << 26) * (uint64_t)blocks) / (uint64_t)(Q.lay.C > 0 ? Q.lay.C : 1);
+        if (max_units < 1) max_units = 1;
         unsigned long long* stats = nullptr;
         if (env_int("VPT_POOL_STATS", 0)) {  /* debug: scheduler statistics, vpt_debug_pool_stats */
             if (!g_pool_stats) HIP_OK(hipMalloc((void**)&g_pool_stats, (TL0 + 3 * TL_MAXWG) * sizeof(unsigned long long)));
@@ -619,7 +678,7 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         const size_t npix = (size_t)K.shard_rows * (size_t)K.w;
         reduce_kernel<FB><<<dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream>>>(Q, K.out);
         HIP_OK(hipGetLastError());
-        return VPT_OK;
+        return slot_done(sl, stream);
     }
     if constexpr (EST <= 1) return launch_wave<EST, COUNT, FB>(ctx, K, stream);
     return VPT_OK;
@@ -636,6 +695,7 @@ static int launch_wave(vpt_context* ctx, KParams K, hipStream_t stream)
     const int need = (tiles + 3) / 4;  /* 4 waves per block, one tile per wave to start */
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
+    std::lock_guard<std::mutex> lock(ctx->mu);
     StreamSlot* sl = nullptr;
     rc = stream_slot(ctx, stream, 0, &sl);
     if (rc) return rc;
@@ -643,7 +703,7 @@ static int launch_wave(vpt_context* ctx, KParams K, hipStream_t stream)
     HIP_OK(hipMemsetAsync(K.queue, 0, sizeof(unsigned), stream));
     render_kernel<EST, COUNT, FB><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(K, S);
     HIP_OK(hipGetLastError());
-    return VPT_OK;
+    return slot_done(sl, stream);
 }
 
 template <bool COUNT>
@@ -710,8 +770,10 @@ void vpt_context_destroy(vpt_context* ctx)
     if (ctx->d_scene) (void)hipFree(ctx->d_scene);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     for (auto& sl : ctx->slots) {
-        if (sl.d_partials) (void)hipFree(sl.d_partials);
-        if (sl.d_queue) (void)hipFree(sl.d_queue);
+        if (sl->done) (void)hipEventSynchronize(sl->done);
+        if (sl->d_partials) (void)hipFree(sl->d_partials);
+        if (sl->d_queue) (void)hipFree(sl->d_queue);
+        if (sl->done) (void)hipEventDestroy(sl->done);
     }
     (void)hipSetDevice(prev);
     delete ctx;
@@ -963,6 +1025,43 @@ int vpt_math_probe(vpt_context* ctx, int fn, const double* x, const double* y, d
     return VPT_OK;
 }
 
+int vpt_phase_probe(vpt_context* ctx, double g, const double din[3], const uint64_t* states, int n, double* dirs,
+                    uint64_t* states_out, const double* wl, int nw, double* values)
+{
+    vpt_clear_error();
+    if (!ctx || !din || n < 0 || nw < 0 || (n > 0 && (!states || !dirs || !states_out)) || (nw > 0 && (!wl || !values)))
+        return vpt_fail(VPT_E_INVALID, "vpt_phase_probe: bad arguments");
+    if (!is_finite(g) || g <= -1.0 || g >= 1.0) return vpt_fail(VPT_E_INVALID, "vpt_phase_probe: g must be in (-1, 1)");
+    const int m = n > nw ? n : nw;
+    if (m == 0) return VPT_OK;
+    HIP_OK(hipSetDevice(ctx->device));
+    uint64_t *dX = nullptr, *dXo = nullptr;
+    double *dd = nullptr, *dw = nullptr, *dv = nullptr;
+    const size_t n1 = (size_t)(n > 0 ? n : 1), w1 = (size_t)(nw > 0 ? nw : 1);
+    hipError_t e = hipMalloc((void**)&dX, n1 * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&dXo, n1 * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&dd, 3 * n1 * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&dw, 3 * w1 * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&dv, w1 * sizeof(double));
+    if (e == hipSuccess && n > 0) e = hipMemcpy(dX, states, (size_t)n * sizeof(uint64_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nw > 0) e = hipMemcpy(dw, wl, 3 * (size_t)nw * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        phase_probe_kernel<<<dim3((unsigned)((m + 255) / 256)), dim3(256)>>>(g, din[0], din[1], din[2], dX, n, dd, dXo, dw,
+                                                                            nw, dv);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && n > 0) e = hipMemcpy(dirs, dd, 3 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && n > 0) e = hipMemcpy(states_out, dXo, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && nw > 0) e = hipMemcpy(values, dv, (size_t)nw * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(dX);
+    (void)hipFree(dXo);
+    (void)hipFree(dd);
+    (void)hipFree(dw);
+    (void)hipFree(dv);
+    if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_phase_probe: %s", hipGetErrorString(e));
+    return VPT_OK;
+}
+
 }  // extern "C"
 
 /* Debug (not part of include/vpt.h): scheduler statistics of the last pool launch made with
@@ -973,6 +1072,23 @@ extern "C" int vpt_debug_pool_stats(unsigned long long* out)
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(out, g_pool_stats, NSTATS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return VPT_OK;
+}
+
+/* debug: the section timers of builds made with -DVPT_SECTIONS=1 (vpt_device.h), 2 x SECT_N
+ * counters (cycles, entries) accumulated since the last call; returns VPT_E_INVALID otherwise */
+extern "C" int vpt_debug_sections(unsigned long long* out)
+{
+#if VPT_SECTIONS
+    if (!out) return VPT_E_INVALID;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(vpt::g_vpt_sect), 2 * vpt::SECT_N * sizeof(unsigned long long)));
+    static const unsigned long long zero[2 * vpt::SECT_N] = {};
+    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(vpt::g_vpt_sect), zero, sizeof(zero)));
+    return VPT_OK;
+#else
+    (void)out;
+    return VPT_E_INVALID;
+#endif
 }
 
 /* debug: the per-workgroup timeline of the last VPT_POOL_STATS launch (vpt_pool.h TL0), 3 x TL_MAXWG */

@@ -69,9 +69,40 @@ int ensure_device_buffer(int device, void** buf, size_t* have, size_t want)
     return VPT_OK;
 }
 
+/* waits for every device's stream (error paths: nothing the call enqueued may still run when it
+ * returns, since the caller may free or reuse what it passed) */
+void sync_all(vpt_multi* m)
+{
+    for (int g = 0; g < m->n; ++g) {
+        if (!m->stream[g]) continue;
+        (void)hipSetDevice(g);
+        (void)hipStreamSynchronize(m->stream[g]);
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+/* The gathered strips -> file order: strip g (at staging + g * slot) holds device g's bands
+ * g, g + n, g + 2n, ... of `band` rows each (the last band may be short), rows of row_bytes.
+ * Exported for tests (not part of include/vpt.h): the n > 1 reassembly runs on the CPU without RCCL. */
+int vpt_debug_band_reorder(const void* staging, size_t slot, int n, int height, int band, size_t row_bytes, void* out)
+{
+    if (!staging || !out || n < 1 || height < 1 || band < 1) return VPT_E_INVALID;
+    const unsigned char* st = (const unsigned char*)staging;
+    unsigned char* o = (unsigned char*)out;
+    const int nbands = (height + band - 1) / band;
+    std::vector<size_t> next(n, 0);  /* next strip row per device */
+    for (int b = 0; b < nbands; ++b) {
+        const int g = b % n, r0 = b * band, r1 = r0 + band < height ? r0 + band : height;
+        for (int fr = r0; fr < r1; ++fr, ++next[g]) {
+            if ((next[g] + 1) * row_bytes > slot) return VPT_E_INVALID;
+            memcpy(o + (size_t)fr * row_bytes, st + (size_t)g * slot + next[g] * row_bytes, row_bytes);
+        }
+    }
+    return VPT_OK;
+}
 
 void vpt_multi_destroy(vpt_multi* m)
 {
@@ -185,7 +216,10 @@ int vpt_multi_render(vpt_multi* m, const vpt_params* p, void* h_out)
         q.band_offset = g;
         void* dst = g == 0 ? m->gather : m->strip[g];
         rc = vpt_render_device(m->ctx[g], &q, dst, (void*)m->stream[g]);
-        if (rc) return rc;
+        if (rc) {
+            sync_all(m);
+            return rc;
+        }
     }
     /* strips -> device 0, slot g (stream-ordered after each render) */
     if (n > 1) {
@@ -198,13 +232,18 @@ int vpt_multi_render(vpt_multi* m, const vpt_params* p, void* h_out)
                 r = ncclRecv((unsigned char*)m->gather + (size_t)g * slot, bytes, ncclUint8, g, m->comm[0], m->stream[0]);
         }
         ncclResult_t r2 = ncclGroupEnd();
-        if (r != ncclSuccess) return nccl_fail("vpt_multi_render: send/recv", r);
-        if (r2 != ncclSuccess) return nccl_fail("vpt_multi_render: ncclGroupEnd", r2);
+        if (r != ncclSuccess || r2 != ncclSuccess) {
+            sync_all(m);
+            return r != ncclSuccess ? nccl_fail("vpt_multi_render: send/recv", r) : nccl_fail("vpt_multi_render: ncclGroupEnd", r2);
+        }
     }
     for (int g = n - 1; g >= 0; --g) {
         hipError_t e = hipSetDevice(g);
         if (e == hipSuccess) e = hipStreamSynchronize(m->stream[g]);
-        if (e != hipSuccess) return hip_fail("vpt_multi_render: synchronize", e);
+        if (e != hipSuccess) {
+            sync_all(m);
+            return hip_fail("vpt_multi_render: synchronize", e);
+        }
     }
     /* gathered strips -> file order */
     if (n == 1) {
@@ -216,14 +255,8 @@ int vpt_multi_render(vpt_multi* m, const vpt_params* p, void* h_out)
     hipError_t e = hipSetDevice(0);
     if (e == hipSuccess) e = hipMemcpy(m->staging.data(), m->gather, slot * (size_t)n, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail("vpt_multi_render: hipMemcpy", e);
-    unsigned char* out = (unsigned char*)h_out;
-    const int nbands = (H + band - 1) / band;
-    std::vector<int> next(n, 0);  /* next strip row per device */
-    for (int b = 0; b < nbands; ++b) {
-        const int g = b % n, r0 = b * band, r1 = r0 + band < H ? r0 + band : H;
-        for (int fr = r0; fr < r1; ++fr, ++next[g])
-            memcpy(out + (size_t)fr * row_bytes, m->staging.data() + (size_t)g * slot + (size_t)next[g] * row_bytes, row_bytes);
-    }
+    if (vpt_debug_band_reorder(m->staging.data(), slot, n, H, band, row_bytes, h_out) != VPT_OK)
+        return vpt_fail(VPT_E_INVALID, "vpt_multi_render: band layout does not fit the strips");
     return VPT_OK;
 }
 

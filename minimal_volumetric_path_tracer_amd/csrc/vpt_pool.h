@@ -59,10 +59,22 @@ namespace vpt {
 #ifndef VPT_LATE_UNIT
 #define VPT_LATE_UNIT 0     /* 1: stage-A-only task fields loaded after the S/M body (A/B: 5674 vs 5757 Ms/s, slower) */
 #endif
+#ifndef VPT_MERGE_LIGHTS
+#define VPT_MERGE_LIGHTS 0  /* bit 0: the diffuse surface rings' code shared by both light kinds; bit 1: the medium rings' */
+#endif
+#ifndef VPT_ONE_A
+#define VPT_ONE_A 0         /* 1: one inlined copy of stage A (ring-A and fused S/M batches share it; A/B FF 53.45 -> 55.29 ms, MIS 260.7 -> 257.8) */
+#endif
+#if VPT_ONE_A && (!VPT_FUSE_A || VPT_LATE_UNIT)
+#error "VPT_ONE_A needs VPT_FUSE_A=1 and VPT_LATE_UNIT=0"
+#endif
 #ifndef VPT_PREP_ROUNDS
 #define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s) */
 #endif
-constexpr int POOL = VPT_POOL_SIZE;  /* task slots per workgroup: 182 B each + ~1.1 KB (161 KB at 880) */
+#ifndef VPT_RING_MASK
+#define VPT_RING_MASK 0x7E  /* register-pressure probes only (wrong images otherwise): bit r compiles the S/M code of ring r */
+#endif
+constexpr int POOL = VPT_POOL_SIZE; /* task slots per workgroup: 182 B each + ~1.1 KB (161 KB at 880) */
 constexpr int NF = 18;      /* doubles per task */
 constexpr int NR = 7;       /* rings */
 constexpr int R_A = 0, R_S = 1, R_M = 5, R_DONE = NR;
@@ -277,6 +289,77 @@ __device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t
     P.partials[o + 2] = t.acc.z;
 }
 
+/* Out-of-line surface events for the rare surface rings (metal, other materials).  Inlined, their
+ * shading (microfacet BSDF in pLight, MISv2 and bdsf; 210 / 145 VGPRs spilled on their own) set the
+ * register allocation of the whole kernel -- 315 VGPRs spilled, whose reloads sit in the hot rings
+ * too.  As a call, their pressure stays inside the callee; the path state crosses through private
+ * temporaries (copied in and out, so the caller's task keeps living in registers). */
+#ifndef VPT_RARE_CALL
+#define VPT_RARE_CALL 0     /* A/B: FF 53.50 -> 61.91 ms, MIS 260.9 -> 303.3 ms (calls force every live value around them) */
+#endif
+#ifndef VPT_RARE_HINT
+#define VPT_RARE_HINT 0     /* A/B: the rare surface rings marked unlikely: 53.50 -> 53.63 ms (no gain) */
+#endif
+template <int EST, bool COUNT, int MK>
+__device__ __attribute__((noinline)) void surface_event_ool(const DevScene* __restrict__ S, Sampler<COUNT>* smp, Path* p,
+                                                            const Event* e, const Medium* m)
+{
+    surface_event<EST, COUNT, MK, -1>(S, *smp, *p, *e, *m);
+}
+
+template <int EST, bool COUNT, int MK>
+__device__ __forceinline__ void surface_event_rare(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
+                                                   const Event& e, const Medium& m)
+{
+#if VPT_RARE_CALL
+    Sampler<COUNT> sm = smp;
+    Path pp = p;
+    Event ee = e;
+    Medium mm = m;
+    surface_event_ool<EST, COUNT, MK>(S, &sm, &pp, &ee, &mm);
+    smp = sm;
+    p = pp;
+#else
+    surface_event<EST, COUNT, MK, -1>(S, smp, p, e, m);
+#endif
+}
+
+/* The S or M event of ring st (1-6) for one task, then the next iteration's roulette draw.  Surface
+ * rings are keyed by material -- diffuse (R_S, R_S + 1), metal (R_S + 2), other -- and by light kind:
+ * sphere light (R_S, R_M), point light (R_S + 1, R_M + 1). */
+#define VPT_RING_ON(r) ((VPT_RING_MASK >> (r)) & 1)
+template <int EST, bool COUNT>
+__device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Task& t, const Medium& m, int st)
+{
+    if constexpr (EST == 5) {  /* iterativePathTracer: the roulette is inside the bounce */
+        if (st == R_S + 2) t.killed = surface_event_pt<COUNT, 1>(S, smp, t.p, t.e);
+        else if (st == R_S) t.killed = surface_event_pt<COUNT, 0>(S, smp, t.p, t.e);
+        else t.killed = surface_event_pt<COUNT, -1>(S, smp, t.p, t.e);
+    } else {
+        SECT_BEGIN(ev);
+        if (st < R_M) {
+            /* metal and other materials: rare (1.4 % of surface events at the bench scene) */
+            if (__builtin_expect(st >= R_S + 2, !VPT_RARE_HINT)) {
+                if (st == R_S + 2) { if (VPT_RING_ON(3)) surface_event_rare<EST, COUNT, 1>(S, smp, t.p, t.e, m); }
+                else { if (VPT_RING_ON(4)) surface_event_rare<EST, COUNT, -1>(S, smp, t.p, t.e, m); }
+            } else if ((VPT_MERGE_LIGHTS & 1) || st == R_S) {
+                /* merged: one copy for both light kinds (the light's radius decides, uniformly per batch) */
+                if (VPT_RING_ON(1)) surface_event<EST, COUNT, 0, (VPT_MERGE_LIGHTS & 1) ? -1 : 0>(S, smp, t.p, t.e, m);
+            } else {
+                if (VPT_RING_ON(2)) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
+            }
+        } else if ((VPT_MERGE_LIGHTS & 2) || st == R_M) {
+            if (VPT_RING_ON(5)) medium_event<EST, COUNT, (VPT_MERGE_LIGHTS & 2) ? -1 : 0>(S, smp, t.p, t.e, m);
+        } else {
+            if (VPT_RING_ON(6)) medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
+        }
+        SECT_END(ev, st < R_M ? SECT_S_TOTAL : SECT_M_TOTAL);
+        SECT_BEGIN(cp);
+        t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
+        SECT_END(cp, SECT_CONT);
+    }
+}
+
 /* Stage A for the lanes with `active`: at most ONE decide() per task.  A converged preparation
  * loop first gives every task a path that has survived its roulette draw.  Lanes that need a
  * work unit take them together from the workgroup's unit ring; a finished unit writes its chunk
@@ -298,6 +381,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         t.killed = false;
     }
     const unsigned long long c0 = dbg_clock(dbg);
+    SECT_BEGIN(pr);
     int round = 0;
     while (true) {
         if (dbg) ++D.rounds;
@@ -322,18 +406,24 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                         __hip_atomic_load(&sh.ctl[C_UTAIL], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - h;
                     got = max(0, min(k, avail));
                 }
-                h = __shfl(h, leader);
-                got = __shfl(got, leader);
-                ex = __shfl(ex, leader);
+                /* leader is wave-uniform: v_readlane, not an LDS permute round trip */
+                h = __builtin_amdgcn_readlane(h, leader);
+                got = __builtin_amdgcn_readlane(got, leader);
+                ex = __builtin_amdgcn_readlane(ex, leader);
                 if (need && r < got) ent = ((volatile uint32_t*)sh.uring)[(h + r) % URING];
                 if (got == 0) break;
+                /* the entry reads above must complete before the claim below: a refill may rewrite
+                 * those positions (mod URING) once uhead has moved past them.  The release fence
+                 * orders them for the compiler and the memory model (one wave's LDS accesses also
+                 * execute in order, which this does not rely on). */
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 int won = 0;
                 if (lane == leader) {
                     int hh = h;
                     won = __hip_atomic_compare_exchange_strong(&sh.uhead, &hh, h + got, __ATOMIC_RELAXED,
                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                if (__shfl(won, leader)) break;
+                if (__builtin_amdgcn_readlane(won, leader)) break;
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (need) {
@@ -396,6 +486,8 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             break;
         }
     }
+    SECT_END(pr, SECT_A_PREP);
+    SECT_BEGIN(cam);
     if (fresh) {  /* camera ray of the surviving sample: src/rt.cpp:787-789 */
         smp.X = t.X;
         const double jx = smp.next();  /* x draw first */
@@ -409,8 +501,10 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         if (EST == 5) t.e.pdf = 1;  /* iterativePathTracer's `factor` rides in the event's pdf slot */
         t.X = smp.X;
     }
+    SECT_END(cam, SECT_A_CAMERA);
     const unsigned long long c1 = dbg_clock(dbg);
     int result = parked ? R_A : R_DONE;
+    SECT_BEGIN(dc);
     if (!done && !parked) {
         smp.X = t.X;
         const int ev = decide<EST>(S, smp, t.p, t.e, m);
@@ -427,6 +521,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             t.e.t = t.e.dist;  /* one slot (F_TD): stage M reads the sampled distance */
         }
     }
+    SECT_END(dc, SECT_A_DECIDE);
     if (dbg) {
         D.c_prep += c1 - c0;
         D.c_decide += dbg_clock(dbg) - c1;
@@ -453,6 +548,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         sh.ticket = sh.serving = 0;
         sh.uhead = 0;
     }
+    sect_init();
     __syncthreads();
 
     Sampler<COUNT> smp;
@@ -469,6 +565,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
     bool seen_exh = false;
     if (dbg && tid == 0) dbg_tl(stats, 0, false);
     while (true) {
+        SECT_BEGIN(sc);
 #if VPT_LOCKFREE
         /* ---- scheduling without a lock (ring_entry): reserve, publish, claim ---- */
         if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(VPT_SCHED_PRIO);
@@ -584,6 +681,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  /* the claimed tasks' states */
         if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(0);
+        SECT_END(sc, SECT_SCHED);
         if (fin) break;
         n = take;
 #else
@@ -701,6 +799,27 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         const bool active = lane < n;
         Task t;
         const int stage = st == R_A ? 0 : st < R_M ? 1 : 2;
+#if VPT_ONE_A
+        /* one copy of stage A in the code: a batch of ring A runs it alone, a batch of an S/M ring
+         * runs its event first and then stage A on the same lanes (VPT_FUSE_A) */
+        SECT_BEGIN(ld);
+        if (active) load_task(sh, slot, t, true);
+        else {
+            t.c1 = 0;
+            t.in_path = false;
+            t.killed = false;
+        }
+        SECT_END(ld, SECT_LOAD);
+        if (stage != 0 && active) {
+            smp.X = t.X;
+            run_event<EST, COUNT>(S, smp, t, m, st);
+            t.X = smp.X;
+        }
+        next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
+        SECT_BEGIN(stt);
+        if (active) store_task(sh, slot, t, true);
+        SECT_END(stt, SECT_STORE);
+#else
         if (stage == 0) {
             if (active) load_task(sh, slot, t, true);
             else {
@@ -714,25 +833,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             if (active) {
                 load_task(sh, slot, t, VPT_FUSE_A != 0 && !VPT_LATE_UNIT);
                 smp.X = t.X;
-                /* surface rings are keyed by material: diffuse (R_S, R_S+1), metal (R_S+2), other */
-                /* and by light kind: sphere light (R_S, R_M), point light (R_S + 1, R_M + 1) */
-                if constexpr (EST == 5) {  /* iterativePathTracer: the roulette is inside the bounce */
-                    if (st == R_S + 2) t.killed = surface_event_pt<COUNT, 1>(S, smp, t.p, t.e);
-                    else if (st == R_S) t.killed = surface_event_pt<COUNT, 0>(S, smp, t.p, t.e);
-                    else t.killed = surface_event_pt<COUNT, -1>(S, smp, t.p, t.e);
-                } else {
-                    if (stage == 1) {
-                        if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m);
-                        else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
-                        else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
-                        else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
-                    } else if (st == R_M) {
-                        medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
-                    } else {
-                        medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
-                    }
-                    t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
-                }
+                run_event<EST, COUNT>(S, smp, t, m, st);
                 t.X = smp.X;
             } else {
                 t.c1 = 0;
@@ -751,6 +852,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             next = R_A;
 #endif
         }
+#endif
         if (dbg) {
             const unsigned long long now = dbg_clock(dbg);
 #pragma unroll
@@ -759,6 +861,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             tclk = now;
         }
     }
+    sect_flush();
     if (COUNT) {
         atomicAdd(&counters[0], (unsigned long long)smp.cnt.tests);
         atomicAdd(&counters[1], (unsigned long long)smp.cnt.iterations);

@@ -243,6 +243,19 @@ class Tracer:
         check(lib().vpt_math_probe(self._ctx, fn, x.ctypes.data, y.ctypes.data, out.ctypes.data, len(x)))
         return out
 
+    def hg_phase(self, g: float, din, states: np.ndarray, wl: np.ndarray):
+        """HG phase extension on the GPU (vpt_phase_probe): (directions sampled around din, end states,
+        phase values toward the rows of wl)."""
+        d = np.ascontiguousarray(din, dtype=np.float64)
+        s = np.ascontiguousarray(states, dtype=np.uint64)
+        w = np.ascontiguousarray(wl, dtype=np.float64).reshape(-1, 3)
+        dirs = np.zeros((len(s), 3))
+        so = np.zeros(len(s), dtype=np.uint64)
+        vals = np.zeros(len(w))
+        check(lib().vpt_phase_probe(self._ctx, float(g), d.ctypes.data, s.ctypes.data, len(s), dirs.ctypes.data,
+                                    so.ctypes.data, w.ctypes.data, len(w), vals.ctypes.data))
+        return dirs, so, vals
+
 
 class MultiTracer:
     """Devices 0 .. n_gpus-1 of THIS process rendering one image together (vpt_multi_*, include/vpt.h):

@@ -95,6 +95,8 @@ class Oracle:
         L.orc_stream_state_c.restype, L.orc_stream_state_c.argtypes = _U, [_U, _U, _U]
         L.orc_is_portable_math.restype = _I
         L.orc_math_n.restype, L.orc_math_n.argtypes = None, [_I, _P, _P, _P, _I]
+        L.orc_hg_phase_sample.restype, L.orc_hg_phase_sample.argtypes = _U, [_D, _P, _U, _P]
+        L.orc_hg_phase_value.restype, L.orc_hg_phase_value.argtypes = _D, [_D, _P, _P]
         self.L = L
         self.portable = bool(L.orc_is_portable_math())
         self.prefix = "orc"
@@ -104,6 +106,21 @@ class Oracle:
         n = len(b) // SPHERE_BYTES
         if self.L.orc_set_scene(b.ctypes.data, n) != 0:
             raise ValueError("oracle: bad scene")
+
+    def hg_phase(self, g: float, din, states: np.ndarray, wl: np.ndarray):
+        """HG extension (phase_sample / phase_value): directions sampled around din from each erand48
+        state, the end states, and the phase values toward the rows of wl."""
+        d = np.ascontiguousarray(din, dtype=np.float64)
+        w = np.ascontiguousarray(wl, dtype=np.float64).reshape(-1, 3)
+        n = len(states)
+        out = np.zeros((n, 3))
+        st = np.zeros(n, dtype=np.uint64)
+        pv = np.zeros(len(w))
+        for i in range(n):
+            st[i] = self.L.orc_hg_phase_sample(g, d.ctypes.data, int(states[i]), out[i].ctypes.data)
+        for i in range(len(w)):
+            pv[i] = self.L.orc_hg_phase_value(g, d.ctypes.data, w[i].ctypes.data)
+        return out, st, pv
 
     def trace(self, estimator: int, rays: np.ndarray, states: np.ndarray, sigma_a=0.001, sigma_s=0.009, hg_g=0.0,
               max_depth=0, counters: bool = False, march_step=0.1, march_light=7):

@@ -276,6 +276,88 @@ def test_overlapping_renders_on_one_context(gpu_tracer):
                 hip.hipStreamDestroy(st)
 
 
+def test_threads_and_many_streams_on_one_context(gpu_tracer):
+    """Several host threads render on different streams of ONE context at once (the context's slot
+    table is taken under its lock until the launches are enqueued; slots have stable addresses), and
+    more streams than the table holds (8) take over finished slots: every image equals the same render
+    done alone."""
+    import ctypes
+    import threading
+
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    ok = lambda rc: rc == 0 or pytest.fail(f"HIP error {rc}")  # noqa: E731
+    gpu_tracer.set_scene(SCENES["default"]())
+    cfgs = [vpt.RenderConfig(width=48 + 8 * i, height=32, spp=6 + i, seed=100 + i, estimator="mis" if i % 3 == 0 else "ff")
+            for i in range(12)]
+    alone = [gpu_tracer.render(c) for c in cfgs]
+    streams = [ctypes.c_void_p() for _ in cfgs]  # 12 streams > the 8 slots of a context
+    bufs = [ctypes.c_void_p() for _ in cfgs]
+    errors = []
+    try:
+        for st in streams:
+            ok(hip.hipStreamCreate(ctypes.byref(st)))
+        for c, b in zip(cfgs, bufs):
+            n = c.height * c.width * 3 * 4
+            ok(hip.hipMalloc(ctypes.byref(b), ctypes.c_size_t(n)))
+            ok(hip.hipMemset(b, 0xFF, ctypes.c_size_t(n)))
+        ok(hip.hipDeviceSynchronize())
+
+        def worker(k):
+            try:
+                for i in range(k, len(cfgs), 4):
+                    for _ in range(2):  # twice on its stream: the slot is reused in stream order
+                        gpu_tracer.render_device(cfgs[i], bufs[i].value, streams[i].value)
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors, errors
+        ok(hip.hipDeviceSynchronize())
+        for a, c, b in zip(alone, cfgs, bufs):
+            got = np.empty((c.height, c.width, 3), dtype=np.float32)
+            ok(hip.hipMemcpy(got.ctypes.data_as(ctypes.c_void_p), b, ctypes.c_size_t(got.nbytes), 2))
+            assert np.array_equal(a, got)
+    finally:
+        hip.hipDeviceSynchronize()
+        for b in bufs:
+            if b.value:
+                hip.hipFree(b)
+        for st in streams:
+            if st.value:
+                hip.hipStreamDestroy(st)
+
+
+def test_band_shards_reassemble_like_multi_render(gpu_tracer):
+    """The n > 1 data path of vpt_multi_render without RCCL: n "devices" render their interleaved
+    row bands (band_stride n, band_offset g) into compact strips, the strips are packed into
+    n slots as the RCCL gather leaves them on device 0, and the library's own reassembly
+    (vpt_debug_band_reorder, the code vpt_multi_render runs) gives the whole image byte for byte."""
+    import ctypes
+
+    L = vpt.lib()
+    L.vpt_debug_band_reorder.restype = ctypes.c_int
+    L.vpt_debug_band_reorder.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_size_t, ctypes.c_void_p]
+    gpu_tracer.set_scene(SCENES["default"]())
+    for n, band, (w, h) in ((2, 16, (64, 96)), (3, 16, (40, 70)), (8, 16, (32, 200)), (8, 5, (24, 53))):
+        whole = gpu_tracer.render(width=w, height=h, spp=4, seed=31)
+        strips = [gpu_tracer.render(width=w, height=h, spp=4, seed=31, band_rows=band, band_stride=n, band_offset=g)
+                  for g in range(n)]
+        row_bytes = w * 3 * 4
+        cap = max(len(s) for s in strips)
+        staging = np.zeros((n, cap, w, 3), dtype=np.float32)
+        for g, st in enumerate(strips):
+            staging[g, :len(st)] = st
+        out = np.full((h, w, 3), np.nan, dtype=np.float32)
+        rc = L.vpt_debug_band_reorder(staging.ctypes.data, cap * row_bytes, n, h, band, row_bytes, out.ctypes.data)
+        assert rc == 0
+        assert out.tobytes() == whole.tobytes(), (n, band)
+
+
 def test_count_work_matches_oracle(gpu_tracer, orc_vm):
     for name in ("default", "mat3", "dielectric"):
         sc = SCENES[name]()
@@ -340,6 +422,25 @@ def test_full_size_properties(gpu_tracer, orc_vm):
     m, ms = img.reshape(-1, 3).mean(0), small.reshape(-1, 3).mean(0)
     se = np.sqrt(img.reshape(-1, 3).var(0) * 8 / img.size * 3 + small.reshape(-1, 3).var(0) * 16 / small.size * 3)
     assert np.all(np.abs(m - ms) <= 6 * se + 1e-6), (m, ms, se)
+
+
+@pytest.mark.gpu
+def test_config1_full_size_256spp_vs_oracle(gpu_tracer, orc_vm):
+    """BASELINE configs[1] at its own size: FF 1024x1024x256 -- the bench workload -- with the auto
+    chunk layout (6 x 32 samples, then the tapered 22, 14, 10, 6, 4, 3, 2, 1, 1, 1: 16 chunks,
+    vpt_chunks.h), which only this sample count exercises at full size.  Six file rows, spread over
+    the image, are recomputed by the oracle (the reference's pixel loop, src/rt.cpp:784-800, with the
+    same per-sample streams and chunked sums) bit for bit; the whole image is finite."""
+    sc = SCENES["default"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    img = gpu_tracer.render(width=1024, height=1024, spp=256, seed=SEED, fp64=True)
+    assert img.shape == (1024, 1024, 3) and np.isfinite(img).all()
+    for fr in (0, 211, 512, 767, 901, 1023):
+        y = 1023 - fr
+        row = orc_vm.render(1024, 1024, 256, 0, seed=SEED, y0=y, y1=y + 1, threads=8)[fr]
+        assert bitwise_equal(img[fr], row).all(), fr
+    assert img.max() > 0
 
 
 # ---------------------------------------------------------------- estimators 2-4 (SURVEY 8f rank 2)
