@@ -39,7 +39,7 @@
 #define VPT_FUSE_RAYS 3
 #endif
 #ifndef VPT_FUSE_RARE_MONO
-#define VPT_FUSE_RARE_MONO 0  /* 1: the fused MISv2 only for diffuse surfaces (MK == 0) */
+#define VPT_FUSE_RARE_MONO 1  /* 1: the fused MISv2 only for diffuse surfaces (MK == 0); with VPT_FR_CALL: scratch 448 -> 240 B/lane, L2 reads 267M -> 129M, FF 51.99 -> 51.53 ms */
 #endif
 /* sphere loops taken G spheres at a time (scene_intersect_grouped): decide() and every other
  * site; A/B at 1024^2 x 256: off 4914, decide only G=5 4967 (G=10 4857), all sites G=5 5042, G=3 5009 */
@@ -56,6 +56,19 @@
 #endif
 
 namespace vpt {
+
+/* branches that are rare at the reference's scenes marked for the compiler (block layout and the
+ * register allocator's spill placement favour the other side); VPT_BRANCH_HINTS=0: no hints */
+#ifndef VPT_BRANCH_HINTS
+#define VPT_BRANCH_HINTS 1
+#endif
+#if VPT_BRANCH_HINTS
+#define VPT_UNLIKELY(c) __builtin_expect(!!(c), 0)
+#define VPT_LIKELY(c) __builtin_expect(!!(c), 1)
+#else
+#define VPT_UNLIKELY(c) (c)
+#define VPT_LIKELY(c) (c)
+#endif
 
 /* timing experiment only (NOT bit-exact): the intersection tests' square roots approximated */
 #ifndef VPT_ISECT_SQRT_APPROX
@@ -78,14 +91,15 @@ namespace vpt {
 enum {
     SECT_SCHED = 0, SECT_LOAD, SECT_S_PLIGHT, SECT_S_MIS, SECT_S_MIS_ISECT, SECT_S_BDSF, SECT_M_SS, SECT_M_SS_DIR,
     SECT_M_SS_ISECT, SECT_M_SS_SHADOW, SECT_M_PHASE, SECT_CONT, SECT_A_PREP, SECT_A_DECIDE, SECT_A_ISECT, SECT_STORE,
-    SECT_S_TOTAL, SECT_M_TOTAL, SECT_A_CAMERA, SECT_USED, SECT_N = 32
+    SECT_S_TOTAL, SECT_M_TOTAL, SECT_A_CAMERA, SECT_A_DECIDE_IN, SECT_M_SHADOW_IN, SECT_A_CAMERA_IN, SECT_USED,
+    SECT_N = 32
 };
 #if VPT_SECTIONS
-__device__ unsigned long long g_vpt_sect[2 * SECT_N];
+__device__ unsigned long long g_vpt_sect[3 * SECT_N];
 __device__ static inline __attribute__((always_inline)) uint32_t* sect_lds()
 {
-    __shared__ uint32_t a[16][2 * SECT_USED];  /* per wave: cycles, entries */
-    return &a[(threadIdx.x >> 6) & 15][0];
+    __shared__ uint32_t a[8][3 * SECT_USED];  /* per wave: cycles, entries, active lanes */
+    return &a[(threadIdx.x >> 6) & 7][0];
 }
 #endif
 __device__ static inline __attribute__((always_inline)) uint32_t sect_now()
@@ -100,11 +114,13 @@ __device__ static inline __attribute__((always_inline)) void sect_add(int k, uin
 {
 #if VPT_SECTIONS
     const uint32_t dt = sect_now() - t0;
-    const int first = __ffsll((unsigned long long)__ballot(1)) - 1;
+    const unsigned long long act = (unsigned long long)__ballot(1);
+    const int first = __ffsll(act) - 1;
     if ((int)(threadIdx.x & 63) == first) {
         uint32_t* a = sect_lds();
         a[k] += dt;
         a[SECT_USED + k] += 1;
+        a[2 * SECT_USED + k] += (uint32_t)__popcll(act);
     }
 #else
     (void)k;
@@ -114,16 +130,17 @@ __device__ static inline __attribute__((always_inline)) void sect_add(int k, uin
 __device__ static inline __attribute__((always_inline)) void sect_init()
 {
 #if VPT_SECTIONS
-    if ((threadIdx.x & 63) < 2 * SECT_USED) sect_lds()[threadIdx.x & 63] = 0;
+    if ((threadIdx.x & 63) < 3 * SECT_USED) sect_lds()[threadIdx.x & 63] = 0;
 #endif
 }
 __device__ static inline __attribute__((always_inline)) void sect_flush()
 {
 #if VPT_SECTIONS
     const int l = threadIdx.x & 63;
-    if (l < 2 * SECT_USED) {
+    if (l < 3 * SECT_USED) {
         const uint32_t v = sect_lds()[l];
-        atomicAdd(&g_vpt_sect[l < SECT_USED ? l : SECT_N + l - SECT_USED], (unsigned long long)v);
+        atomicAdd(&g_vpt_sect[l < SECT_USED ? l : l < 2 * SECT_USED ? SECT_N + l - SECT_USED : 2 * SECT_N + l - 2 * SECT_USED],
+                  (unsigned long long)v);
     }
 #endif
 }
@@ -572,7 +589,7 @@ VPT_DEV double microfacet_prob(dv3 wo, dv3 wh, double alpha, dv3 n)
  * channels, two Smith terms and the NDF are independent chains that the scheduler interleaves, and
  * inlined at the five sites of a metal surface event they set the kernel's register allocation. */
 #ifndef VPT_FR_CALL
-#define VPT_FR_CALL 0       /* A/B (with VPT_FUSE_RARE_MONO): 53.28 vs 53.50 ms FF, 263.5 vs 260.9 MIS */
+#define VPT_FR_CALL 1       /* with VPT_FUSE_RARE_MONO (A/B above); round-2 tree: 53.28 vs 53.50 ms FF */
 #endif
 #if VPT_FR_CALL
 #define VPT_FR_QUAL __device__ static __attribute__((noinline))
@@ -1006,7 +1023,7 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
     dv3 Le;
     if (visibility(S, smp, light, x, false, lr, l3)) {
         Le = scl(I, (1 / (dot(sub(light, x), sub(light, x)))));
-    } else if (S->n_mat3 == 0) {
+    } else if (VPT_LIKELY(S->n_mat3 == 0)) {
         smp.tests(S->n);  /* visibilityVPT == visibility (no material-3 sphere): same miss */
         Le = mk(0, 0, 0);
     } else if (visibility(S, smp, light, x, true, lr, l3)) {
@@ -1070,6 +1087,7 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         if (with_sigma) Ld = scl(scl(scl(scl(Ls, trxt), sigma_s), (1 / prob_wl)), (1 / probSource));
         else Ld = scl(scl(Ls, (1 / prob_wl)), (1 / probSource));
     } else if (point) {
+        SECT_BEGIN(swi);
         if (visibility(S, smp, lp, xt, false, -1.0, false)) {
             double distanceLight = dot(sub(lp, xt), sub(lp, xt));
             dv3 Le = scl(rad, (1 / distanceLight));
@@ -1078,6 +1096,7 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
             if (with_sigma) Ld = scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
             else Ld = scl(Ls, (1 / probSource));
         }
+        SECT_END(swi, SECT_M_SHADOW_IN);
     }
     SECT_END(sw, SECT_M_SS_SHADOW);
     return Ld;
@@ -1200,7 +1219,7 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
         return EV_SURF;
     }
     const int count = S->n_emit;
-    if (count == 0) return EV_END;
+    if (VPT_UNLIKELY(count == 0)) return EV_END;
     e.src = S->emit[(int)(smp.next() * count)];
     bool surf;
     if (est_free_flight<EST>()) {

@@ -38,6 +38,17 @@
 #endif
 #include "vpt_glibm_tables.h"
 
+/* the rare arguments' branches (the translated library functions) marked unlikely, so that the
+ * register allocator and the block layout serve the common path (VPT_LIBM_HINT=0: no hint) */
+#ifndef VPT_LIBM_HINT
+#define VPT_LIBM_HINT 1
+#endif
+#if VPT_LIBM_HINT
+#define GM_UNLIKELY(c) __builtin_expect(!!(c), 0)
+#else
+#define GM_UNLIKELY(c) (c)
+#endif
+
 VM_QUAL int32_t gm_hi(double x) { return (int32_t)(vm_as_u64(x) >> 32); }
 VM_QUAL uint32_t gm_lo(double x) { return (uint32_t)vm_as_u64(x); }
 VM_QUAL double gm_fma(double a, double b, double c) { return fma(a, b, c); }
@@ -358,7 +369,7 @@ VM_QUAL double gm_exp(double x)
     const double tmp = gm_fma(r2 * r2, p45, gm_fma(p23, r2, r + tail));
     const double scale = vm_as_f64(sbits);
     double v = gm_fma(scale, tmp, scale);
-    if (abstop - 0x3c9u >= 0x3fu) v = gl_exp(x);
+    if (GM_UNLIKELY(abstop - 0x3c9u >= 0x3fu)) v = gl_exp(x);
     return v;
 }
 
@@ -406,7 +417,7 @@ VM_QUAL double gm_log(double x)
     q = gm_fma(q, r2, gm_fma(r, VM_T(K, GL_A0), VM_T(K, GL_A1)));
     const double v2 = gm_fma(r * r2, q, lo) + hi;
     double v = ix + 0xc012000000000000ull <= 0x308ffffffffffull ? v1 : v2;
-    if (top - 0x0010u >= 0x7ff0u - 0x0010u) v = gl_log(x);
+    if (GM_UNLIKELY(top - 0x0010u >= 0x7ff0u - 0x0010u)) v = gl_log(x);
     return v;
 }
 
@@ -473,7 +484,7 @@ VM_QUAL double gm_atan2(double y, double x)
     const double tm500 = VM_T(K, GT_TM500), t500 = VM_T(K, GT_T500);
     const int rare = !(x > 0.0) || !(ay > 0.0) || !(x < __builtin_inf()) || !(ay < __builtin_inf()) ||
                      de < -0x38fffff || ax < tm500 || ay < tm500 || ax > t500 || ay > t500;
-    if (rare) r = gl_atan2(y, x);
+    if (GM_UNLIKELY(rare)) r = gl_atan2(y, x);
     return r;
 }
 

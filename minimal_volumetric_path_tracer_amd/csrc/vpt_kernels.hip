@@ -1074,15 +1074,15 @@ extern "C" int vpt_debug_pool_stats(unsigned long long* out)
     return VPT_OK;
 }
 
-/* debug: the section timers of builds made with -DVPT_SECTIONS=1 (vpt_device.h), 2 x SECT_N
- * counters (cycles, entries) accumulated since the last call; returns VPT_E_INVALID otherwise */
+/* debug: the section timers of builds made with -DVPT_SECTIONS=1 (vpt_device.h), 3 x SECT_N
+ * counters (cycles, entries, active lanes) accumulated since the last call; returns VPT_E_INVALID otherwise */
 extern "C" int vpt_debug_sections(unsigned long long* out)
 {
 #if VPT_SECTIONS
     if (!out) return VPT_E_INVALID;
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(vpt::g_vpt_sect), 2 * vpt::SECT_N * sizeof(unsigned long long)));
-    static const unsigned long long zero[2 * vpt::SECT_N] = {};
+    HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(vpt::g_vpt_sect), 3 * vpt::SECT_N * sizeof(unsigned long long)));
+    static const unsigned long long zero[3 * vpt::SECT_N] = {};
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(vpt::g_vpt_sect), zero, sizeof(zero)));
     return VPT_OK;
 #else

@@ -59,14 +59,23 @@ namespace vpt {
 #ifndef VPT_LATE_UNIT
 #define VPT_LATE_UNIT 0     /* 1: stage-A-only task fields loaded after the S/M body (A/B: 5674 vs 5757 Ms/s, slower) */
 #endif
+#ifndef VPT_SHFL_LEADER
+#define VPT_SHFL_LEADER 0   /* 1: stage A's unit-ring leader values broadcast by __shfl (LDS permute), 0: v_readlane */
+#endif
+#ifndef VPT_RUN_EVENT_ORDER
+#define VPT_RUN_EVENT_ORDER 0  /* 1: the rare surface rings tested first (with VPT_RARE_HINT); 0: index order (A/B 55.71 ms / 269.8) */
+#endif
 #ifndef VPT_MERGE_LIGHTS
 #define VPT_MERGE_LIGHTS 0  /* bit 0: the diffuse surface rings' code shared by both light kinds; bit 1: the medium rings' */
 #endif
 #ifndef VPT_ONE_A
-#define VPT_ONE_A 0         /* 1: one inlined copy of stage A (ring-A and fused S/M batches share it; A/B FF 53.45 -> 55.29 ms, MIS 260.7 -> 257.8) */
+#define VPT_ONE_A 1         /* 1: one inlined copy of stage A (ring-A and fused S/M batches share it; A/B FF 53.45 -> 55.29 ms, MIS 260.7 -> 257.8) */
 #endif
 #if VPT_ONE_A && (!VPT_FUSE_A || VPT_LATE_UNIT)
 #error "VPT_ONE_A needs VPT_FUSE_A=1 and VPT_LATE_UNIT=0"
+#endif
+#ifndef VPT_PREP_TRIES
+#define VPT_PREP_TRIES 2    /* samples a lane may start per preparation round (A/B 1 / 2 / 4 / 8: FF 52.16 / 52.02 / 53.70 / 53.85 ms, MIS 248.1 / 245.2 / 251.9 / 252.0) */
 #endif
 #ifndef VPT_PREP_ROUNDS
 #define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s) */
@@ -298,7 +307,7 @@ __device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t
 #define VPT_RARE_CALL 0     /* A/B: FF 53.50 -> 61.91 ms, MIS 260.9 -> 303.3 ms (calls force every live value around them) */
 #endif
 #ifndef VPT_RARE_HINT
-#define VPT_RARE_HINT 0     /* A/B: the rare surface rings marked unlikely: 53.50 -> 53.63 ms (no gain) */
+#define VPT_RARE_HINT 0     /* the rare surface rings marked unlikely (A/B with VPT_RUN_EVENT_ORDER=1: FF 56.68 -> 53.95 ms, MIS 275.7 -> 259.4) */
 #endif
 template <int EST, bool COUNT, int MK>
 __device__ __attribute__((noinline)) void surface_event_ool(const DevScene* __restrict__ S, Sampler<COUNT>* smp, Path* p,
@@ -339,7 +348,12 @@ __device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sample
         SECT_BEGIN(ev);
         if (st < R_M) {
             /* metal and other materials: rare (1.4 % of surface events at the bench scene) */
-            if (__builtin_expect(st >= R_S + 2, !VPT_RARE_HINT)) {
+            if (!VPT_RUN_EVENT_ORDER) {  /* round-2 order: the rings in index order */
+                if (st == R_S) { if (VPT_RING_ON(1)) surface_event<EST, COUNT, 0, (VPT_MERGE_LIGHTS & 1) ? -1 : 0>(S, smp, t.p, t.e, m); }
+                else if (st == R_S + 1) { if (VPT_RING_ON(2)) surface_event<EST, COUNT, 0, (VPT_MERGE_LIGHTS & 1) ? -1 : 1>(S, smp, t.p, t.e, m); }
+                else if (st == R_S + 2) { if (VPT_RING_ON(3)) surface_event_rare<EST, COUNT, 1>(S, smp, t.p, t.e, m); }
+                else { if (VPT_RING_ON(4)) surface_event_rare<EST, COUNT, -1>(S, smp, t.p, t.e, m); }
+            } else if (VPT_RARE_HINT ? __builtin_expect(st >= R_S + 2, 0) : st >= R_S + 2) {
                 if (st == R_S + 2) { if (VPT_RING_ON(3)) surface_event_rare<EST, COUNT, 1>(S, smp, t.p, t.e, m); }
                 else { if (VPT_RING_ON(4)) surface_event_rare<EST, COUNT, -1>(S, smp, t.p, t.e, m); }
             } else if ((VPT_MERGE_LIGHTS & 1) || st == R_S) {
@@ -407,9 +421,15 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                     got = max(0, min(k, avail));
                 }
                 /* leader is wave-uniform: v_readlane, not an LDS permute round trip */
+#if VPT_SHFL_LEADER
+                h = __shfl(h, leader);
+                got = __shfl(got, leader);
+                ex = __shfl(ex, leader);
+#else
                 h = __builtin_amdgcn_readlane(h, leader);
                 got = __builtin_amdgcn_readlane(got, leader);
                 ex = __builtin_amdgcn_readlane(ex, leader);
+#endif
                 if (need && r < got) ent = ((volatile uint32_t*)sh.uring)[(h + r) % URING];
                 if (got == 0) break;
                 /* the entry reads above must complete before the claim below: a refill may rewrite
@@ -453,10 +473,11 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             }
         }
         if (!done && !parked && !t.in_path && t.c1 != 0) {
-            if (t.i == t.c1) {
-                store_partial(P, t);
-                t.c1 = 0;
-            } else {
+            /* up to VPT_PREP_TRIES samples of the unit per round: a sample killed by its first
+             * roulette draw costs only its stream start (no LDS, no hand-out), so trying the next
+             * one here instead of in the next round keeps the lane from parking (a parked lane
+             * idles through this batch's decide) */
+            for (int k = 0; k < VPT_PREP_TRIES && !t.in_path && t.i != t.c1; ++k) {
                 const uint64_t X0 = vpt_stream_start_key(t.key, (uint64_t)t.i);  /* key: src/rt.cpp:773 idx */
                 ++t.i;
                 if (dbg) ++D.samples;
@@ -476,6 +497,10 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                     }
                 }
             }
+            if (VPT_UNLIKELY(!t.in_path && t.i == t.c1)) {  /* the unit is done: its chunk sum out */
+                store_partial(P, t);
+                t.c1 = 0;
+            }
         }
         if (__ballot(!done && !parked && !t.in_path) == 0) break;
         /* a lane still without a path after VPT_PREP_ROUNDS rounds is parked (back to ring A, it
@@ -489,6 +514,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
     SECT_END(pr, SECT_A_PREP);
     SECT_BEGIN(cam);
     if (fresh) {  /* camera ray of the surviving sample: src/rt.cpp:787-789 */
+        SECT_BEGIN(ci);
         smp.X = t.X;
         const double jx = smp.next();  /* x draw first */
         const double jy = smp.next();
@@ -500,12 +526,14 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         t.p.depth = 0;
         if (EST == 5) t.e.pdf = 1;  /* iterativePathTracer's `factor` rides in the event's pdf slot */
         t.X = smp.X;
+        SECT_END(ci, SECT_A_CAMERA_IN);
     }
     SECT_END(cam, SECT_A_CAMERA);
     const unsigned long long c1 = dbg_clock(dbg);
     int result = parked ? R_A : R_DONE;
     SECT_BEGIN(dc);
     if (!done && !parked) {
+        SECT_BEGIN(dci);
         smp.X = t.X;
         const int ev = decide<EST>(S, smp, t.p, t.e, m);
         t.X = smp.X;
@@ -520,6 +548,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             result = R_M + (EST == 3 ? 0 : S->geo[t.e.src].point);
             t.e.t = t.e.dist;  /* one slot (F_TD): stage M reads the sampled distance */
         }
+        SECT_END(dci, SECT_A_DECIDE_IN);
     }
     SECT_END(dc, SECT_A_DECIDE);
     if (dbg) {
@@ -596,8 +625,8 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                 seen_exh = true;
                 if (lane == 0) dbg_tl(stats, 1, false);
             }
-            if (!__builtin_amdgcn_readlane(v, C_EXH) && !__builtin_amdgcn_readlane(v, C_RFL) &&
-                __builtin_amdgcn_readlane(v, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL) {
+            if (VPT_UNLIKELY(!__builtin_amdgcn_readlane(v, C_EXH) && !__builtin_amdgcn_readlane(v, C_RFL) &&
+                __builtin_amdgcn_readlane(v, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL)) {
                 int own = 0;
                 if (lane == 0) {
                     int z = 0;
@@ -640,7 +669,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                     st = r;
                 }
             }
-            if (best <= 0) {
+            if (VPT_UNLIKELY(best <= 0)) {
                 if (__builtin_amdgcn_readlane(v, C_DONE) == POOL) {
                     fin = true;
                     break;
@@ -660,7 +689,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             }
             const uint64_t okm = __ballot(ok);
             const int got = okm == ~0ull ? 64 : __builtin_ctzll(~okm);  /* the published prefix */
-            if (got == 0) {
+            if (VPT_UNLIKELY(got == 0)) {
                 ++st_retry;
                 __builtin_amdgcn_s_sleep(1);
                 continue;
@@ -671,7 +700,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                 won = __hip_atomic_compare_exchange_strong(&sh.ctl[C_HEAD + st], &hh, h + got, __ATOMIC_RELAXED,
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            if (!__builtin_amdgcn_readfirstlane(won)) {
+            if (VPT_UNLIKELY(!__builtin_amdgcn_readfirstlane(won))) {
                 ++st_retry;
                 continue;
             }

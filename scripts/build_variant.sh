@@ -8,7 +8,7 @@ name=$1
 shift
 mkdir -p build_variants
 C=minimal_volumetric_path_tracer_amd/csrc
-make -s -C "$C" vpt_host.o vpt_multi.o vpt_build_id.o
+flock /tmp/vpt_build_variant.lock make -s -C "$C" vpt_host.o vpt_multi.o vpt_build_id.o
 /opt/rocm/bin/hipcc --offload-arch=${VARCH:-gfx950} -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
     -Wno-unused-function "$@" -c "$C/vpt_kernels.hip" -o "build_variants/vpt_kernels_$name.o"
 /opt/rocm/bin/hipcc --offload-arch=${VARCH:-gfx950} -shared -fPIC "build_variants/vpt_kernels_$name.o" "$C/vpt_host.o" "$C/vpt_multi.o" "$C/vpt_build_id.o" \

@@ -6,14 +6,14 @@ import minimal_volumetric_path_tracer_amd as vpt
 
 NAMES = ["sched", "load_task", "S pLight", "S MISv2", "S MISv2 isect3", "S bdsf+update", "M single_scat", "M ss cone dir",
          "M ss cone isect", "M ss shadow/Ld", "M phase", "roulette", "A prep", "A decide", "A decide isect", "store_task",
-         "S total", "M total", "A camera"]
+         "S total", "M total", "A camera", "A decide (in)", "M shadow (in)", "A camera (in)"]
 N = 32
 t = vpt.Tracer(0)
 est = sys.argv[1] if len(sys.argv) > 1 else "ff"
 g = float(sys.argv[2]) if len(sys.argv) > 2 else (0.5 if est == "mis" else 0.0)
 spp = 256 if est == "ff" else 128
 t.render(width=64, height=64, spp=4, estimator=est, hg_g=g)
-buf = (ctypes.c_ulonglong * (2 * N))()
+buf = (ctypes.c_ulonglong * (3 * N))()
 vpt.lib().vpt_debug_sections(buf)
 t0 = time.time()
 t.render(width=1024, height=1024, spp=spp, estimator=est, hg_g=g)
@@ -25,4 +25,4 @@ print(f"{est} g={g} 1024x1024x{spp}: {dt*1e3:.1f} ms (instrumented); top-level w
 for k, name in enumerate(NAMES):
     c, n = s[k], s[N + k]
     if n:
-        print(f"  {name:16s} share {c/top:6.3f}  entries {n:10d}  cycles/entry {c/n:8.0f}")
+        print(f"  {name:16s} share {c/top:6.3f}  entries {n:10d}  cycles/entry {c/n:8.0f}  lanes/entry {s[2 * N + k]/n:5.1f}")
