@@ -1,6 +1,9 @@
 /*
  * vpt_glibm.h -- the reference's transcendentals, bit for bit, on the GPU.
  *
+ * Restates algorithms of the GNU C Library (glibc 2.35, sysdeps/ieee754/dbl-64): LGPL-2.1-or-later,
+ * see LICENSE-glibc-derived.md (how libvpt.so is rebuilt from these sources).
+ *
  * The reference calls glibc's libm (include/samplingFunctions.h:47-82 acos/sin/cos,
  * include/vptSamplingFunctions.h:11-62 log/acos/sin/cos/tan, include/microFacetUtilities.h:34-84
  * atan/log/exp, include/volumetricBasicFunctions.h:14-21,209-223 exp/atan2), and several

@@ -549,7 +549,8 @@ def main():
     with open(args.out, "w") as fh:
         w = fh.write
         w("/* GENERATED by scripts/gen_glibc_libm.py from libm.so.6 build-id %s (Ubuntu GLIBC\n" % BUILD_ID)
-        w(" * 2.35-0ubuntu3.12), x86-64 FMA variants.  Do not edit.  GNU C Library, LGPL-2.1-or-later.\n")
+        w(" * 2.35-0ubuntu3.12), x86-64 FMA variants.  Do not edit.  GNU C Library, LGPL-2.1-or-later\n")
+        w(" * (LICENSE-glibc-derived.md: the notice and how libvpt.so is rebuilt from these sources).\n")
         w(" *\n * gl_exp, gl_log, gl_sin, gl_cos, gl_tan, gl_atan, gl_acos, gl_atan2: the same bits as the\n")
         w(" * reference's libm calls for every argument the tracer passes (tests/test_glibc_libm.py).\n")
         w(" * Register variables r_* (integer) and x* (low lane of xmm*, as bits); flags zf/cf/sf/of/pf.\n */\n")

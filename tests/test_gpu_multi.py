@@ -89,6 +89,28 @@ def test_cli_default_float32_framebuffer(orc_vm, tmp_path):
     assert (tmp_path / "image.ppm").read_bytes() == (tmp_path / "o.ppm").read_bytes()
 
 
+@pytest.mark.parametrize("prog", ["rt_vpt", "rt_vpt_multi"])
+def test_integration_dropin_program_runs(tmp_path, prog):
+    """INTEGRATION.md section 1 executed: the reference's own main() (src/rt.cpp) with the drop-in
+    blocks in place of its pixel loop and PPM writer, built by __graft_entry__.build() from a copy of
+    the reference sources (oracle/dropin.py).  `rt_vpt 2` renders the reference's 1024x768 image at
+    2 spp through vpt_render (rt_vpt_multi: vpt_render_multi over every GPU present), prints the
+    reference's timing line and writes image.ppm -- byte-identical to the library's own render of
+    the same default parameters encoded by the PPM writer."""
+    exe = os.path.join(ROOT, "oracle", "_ref", prog)
+    if not os.path.exists(exe):
+        pytest.skip(f"{exe} not built (needs the reference checkout at build time)")
+    r = subprocess.run([exe, "2"], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert re.search(r"elapsed time: [0-9.e+-]+s", r.stdout), r.stdout[-500:]
+    t = vpt.Tracer(0)
+    try:
+        img = t.render(vpt.RenderConfig(width=1024, height=768, spp=2))
+    finally:
+        t.close()
+    assert (tmp_path / "image.ppm").read_bytes() == vpt.encode_ppm(img)
+
+
 def test_cli_rejects_bad_arguments(tmp_path):
     for args in (["x"], ["0"], ["4", "--estimator", "nope"], ["4", "--gpus", "0"], ["4", "--width"]):
         r = subprocess.run([VPT] + args, cwd=tmp_path, capture_output=True, text=True, timeout=60)
