@@ -35,7 +35,6 @@ struct vpt_multi {
     std::vector<size_t> strip_bytes;
     void* gather = nullptr;             /* on device 0: n slots of `slot_bytes` */
     size_t gather_bytes = 0;
-    std::vector<unsigned char> staging; /* host copy of the gathered strips */
 };
 
 namespace {
@@ -84,23 +83,45 @@ void sync_all(vpt_multi* m)
 
 extern "C" {
 
-/* The gathered strips -> file order: strip g (at staging + g * slot) holds device g's bands
- * g, g + n, g + 2n, ... of `band` rows each (the last band may be short), rows of row_bytes.
- * Exported for tests (not part of include/vpt.h): the n > 1 reassembly runs on the CPU without RCCL. */
-int vpt_debug_band_reorder(const void* staging, size_t slot, int n, int height, int band, size_t row_bytes, void* out)
+}  // extern "C"
+
+namespace {
+
+/* The gathered strips -> file order, as copies: strip g (at g * slot of the gather buffer) holds
+ * device g's bands g, g + n, g + 2n, ... of `band` rows each (the last band may be short), rows of
+ * row_bytes, so band b is ONE contiguous run in both the strip and the file.  Returns false when a
+ * strip would overrun its slot. */
+struct BandCopy {
+    size_t src, dst, bytes;
+};
+bool band_plan(size_t slot, int n, int height, int band, size_t row_bytes, std::vector<BandCopy>& plan)
 {
-    if (!staging || !out || n < 1 || height < 1 || band < 1) return VPT_E_INVALID;
-    const unsigned char* st = (const unsigned char*)staging;
-    unsigned char* o = (unsigned char*)out;
+    plan.clear();
     const int nbands = (height + band - 1) / band;
     std::vector<size_t> next(n, 0);  /* next strip row per device */
     for (int b = 0; b < nbands; ++b) {
         const int g = b % n, r0 = b * band, r1 = r0 + band < height ? r0 + band : height;
-        for (int fr = r0; fr < r1; ++fr, ++next[g]) {
-            if ((next[g] + 1) * row_bytes > slot) return VPT_E_INVALID;
-            memcpy(o + (size_t)fr * row_bytes, st + (size_t)g * slot + next[g] * row_bytes, row_bytes);
-        }
+        const size_t rows = (size_t)(r1 - r0);
+        if ((next[g] + rows) * row_bytes > slot) return false;
+        plan.push_back({(size_t)g * slot + next[g] * row_bytes, (size_t)r0 * row_bytes, rows * row_bytes});
+        next[g] += rows;
     }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+/* The reassembly plan of vpt_multi_render applied on the host (staging = the gather buffer's bytes).
+ * Exported for tests (not part of include/vpt.h): the n > 1 layout is checked on the CPU without
+ * RCCL; vpt_multi_render applies the same plan with device-to-host copies. */
+int vpt_debug_band_reorder(const void* staging, size_t slot, int n, int height, int band, size_t row_bytes, void* out)
+{
+    if (!staging || !out || n < 1 || height < 1 || band < 1) return VPT_E_INVALID;
+    std::vector<BandCopy> plan;
+    if (!band_plan(slot, n, height, band, row_bytes, plan)) return VPT_E_INVALID;
+    for (const BandCopy& c : plan) memcpy((unsigned char*)out + c.dst, (const unsigned char*)staging + c.src, c.bytes);
     return VPT_OK;
 }
 
@@ -251,12 +272,20 @@ int vpt_multi_render(vpt_multi* m, const vpt_params* p, void* h_out)
         if (e != hipSuccess) return hip_fail("vpt_multi_render: hipMemcpy", e);
         return VPT_OK;
     }
-    m->staging.resize(slot * (size_t)n);
-    hipError_t e = hipSetDevice(0);
-    if (e == hipSuccess) e = hipMemcpy(m->staging.data(), m->gather, slot * (size_t)n, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return hip_fail("vpt_multi_render: hipMemcpy", e);
-    if (vpt_debug_band_reorder(m->staging.data(), slot, n, H, band, row_bytes, h_out) != VPT_OK)
+    /* each band straight from the gather buffer into its file rows (no host staging, no host
+     * reorder pass): one device-to-host copy per band, queued back to back on device 0's stream */
+    std::vector<BandCopy> plan;
+    if (!band_plan(slot, n, H, band, row_bytes, plan))
         return vpt_fail(VPT_E_INVALID, "vpt_multi_render: band layout does not fit the strips");
+    hipError_t e = hipSetDevice(0);
+    for (size_t i = 0; i < plan.size() && e == hipSuccess; ++i)
+        e = hipMemcpyAsync((unsigned char*)h_out + plan[i].dst, (const unsigned char*)m->gather + plan[i].src, plan[i].bytes,
+                           hipMemcpyDeviceToHost, m->stream[0]);
+    if (e == hipSuccess) e = hipStreamSynchronize(m->stream[0]);
+    if (e != hipSuccess) {
+        sync_all(m);
+        return hip_fail("vpt_multi_render: device-to-host copy", e);
+    }
     return VPT_OK;
 }
 
