@@ -1102,10 +1102,11 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     return Ld;
 }
 
-/* equiAngularParams2 (include/volumetricBasicFunctions.h:209-223) */
-template <bool COUNT>
-VPT_DEV double equiangular_params2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int src, double tMax, dv3 ro,
-                                   dv3 rd, double& D, double& ta, double& tb, double& sample_t)
+/* equiAngularParams2 (include/volumetricBasicFunctions.h:209-223) with its one draw x given: every
+ * other operand is a function of the ray, the light and tMax, so the draw can be taken earlier in the
+ * stream's order (it is the stream's next draw either way) and the arithmetic done later */
+VPT_DEV double equiangular_setup(const DevScene* __restrict__ S, int src, double tMax, dv3 ro, dv3 rd, double x,
+                                 double& D, double& ta, double& tb, double& sample_t)
 {
     dv3 dv = sub(sph_p(S, src), ro);
     double dvn = vm_sqrt(dot(dv, dv));
@@ -1113,10 +1114,28 @@ VPT_DEV double equiangular_params2(const DevScene* __restrict__ S, Sampler<COUNT
     D = vm_sqrt(dvn * dvn - proj * proj);
     ta = lm_atan2(0.0 - proj, D);
     tb = lm_atan2(tMax - proj, D);
-    double x = smp.next();
     sample_t = D * lm_tan((1 - x) * ta + x * tb);
     return sample_t + proj;
 }
+
+template <bool COUNT>
+VPT_DEV double equiangular_params2(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int src, double tMax, dv3 ro,
+                                   dv3 rd, double& D, double& ta, double& tb, double& sample_t)
+{
+    const double x = smp.next();
+    return equiangular_setup(S, src, tMax, ro, rd, x, D, ta, tb, sample_t);
+}
+
+/* Equi-angular estimators (1, 4): decide() takes the distance draw and the surface coin, and the
+ * equi-angular arithmetic (two atan2, a tan, the pdf) runs in the medium event only -- a surface
+ * event (a third of them) never reads it.  The draw rides in Event::pdf, its sign bit marking a
+ * ray that hit nothing (EST 4's psurf is 0 there). */
+#ifndef VPT_PLIGHT_SKIP
+#define VPT_PLIGHT_SKIP 1   /* surface_event: pLight toward a sphere light skipped when exactly zero in every lane */
+#endif
+#ifndef VPT_EQA_DEFER
+#define VPT_EQA_DEFER 1
+#endif
 
 /* equiAngularProb, include/vptSamplingFunctions.h:60-62 */
 VPT_DEV double equiangular_prob(double D, double ta, double tb, double s) { return D / vm_fabs(tb - ta) / (s * s + D * D); }
@@ -1226,12 +1245,17 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
         e.dist = -lm_log(1 - smp.next()) / sigma_t;  /* freeFlightSample, vptSamplingFunctions.h:11-14 */
         surf = e.dist > t;
     } else {
-        double D = 0, ta = 0, tb = 0, sd = 0;
         /* MIS: psurf = exp(-σt t) (:1419); explicit: TrActual = Tr(x, xs), 0 on a miss (:1033-1041) */
         const double psurf = EST == 1 ? lm_exp(sigma_t * t * -1.0)
                                       : (hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0);
-        e.dist = equiangular_params2(S, smp, e.src, t, p.o, p.d, D, ta, tb, sd);
-        e.pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
+        if (VPT_EQA_DEFER) {
+            const double x = smp.next();  /* equiAngularParams2's draw (volumetricBasicFunctions.h:219) */
+            e.pdf = hit ? x : -x;          /* medium_event: eqa_medium */
+        } else {
+            double D = 0, ta = 0, tb = 0, sd = 0;
+            e.dist = equiangular_params2(S, smp, e.src, t, p.o, p.d, D, ta, tb, sd);
+            e.pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
+        }
         surf = EST == 1 ? smp.next() < psurf : smp.next() <= psurf;  /* :1423 / :1096 */
     }
     if (!surf) return EV_MED;
@@ -1267,8 +1291,27 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     const double probSource = 1.0 / S->n_emit;
     const double alpha = S->sph[id].alpha;
     SECT_BEGIN(pl);
-    double Trs = transmitance(xs, sph_p(S, src), sigma_t);
-    dv3 Ldp = scl(scl(p_light<COUNT, MK, PT>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+    dv3 Ldp = mk(0, 0, 0);
+    /* pLight toward a sphere light (PT == 0: the pool's ring) is exactly zero unless x lies inside
+     * the light (the shadow ray from the light's centre ends on the light's own surface):
+     * Le = 0, and Le fr cos Trs / probSource is then +-0 whenever its other factors are finite --
+     * which the distance and the normal decide.  Ld (MISv2) is never -0 (its sums start at +0), so
+     * Ldp + Ld == Ld: when that holds in every lane of the wave, the frames, the normalisations and
+     * the transmittance of pLight are skipped -- same bits, no draws involved. */
+    bool plight_zero = false;
+    if (VPT_PLIGHT_SKIP && PT == 0 && S->n_mat3 == 0) {
+        const dv3 lx = sub(sph_p(S, src), xs);
+        const double dd = dot(lx, lx);
+        const double distance = vm_sqrt(dd);  /* visibility()'s test, pathTracingUtilities.h:44-51 */
+        const bool fin = dd > 0 && dd < VPT_DBL_MAX && nx.x - nx.x == 0 && nx.y - nx.y == 0 && nx.z - nx.z == 0;
+        const bool zero = S->sph[src].r > 0.0001 && !(distance < S->sph[src].r) && fin;
+        plight_zero = __ballot(!zero) == 0;
+        if (plight_zero) smp.tests(2 * S->n);  /* what visibility + the visibilityVPT miss would count */
+    }
+    if (!plight_zero) {
+        double Trs = transmitance(xs, sph_p(S, src), sigma_t);
+        Ldp = scl(scl(p_light<COUNT, MK, PT>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+    }
     SECT_END(pl, SECT_S_PLIGHT);
     SECT_BEGIN(mis);
 #if VPT_FUSE_RAYS
@@ -1330,13 +1373,31 @@ VPT_DEV bool surface_event_pt(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     return false;
 }
 
+/* the deferred equi-angular arithmetic of decide() (VPT_EQA_DEFER): d_final and its pdf from the
+ * ray, the light, tMax = e.t and the draw carried in e.pdf -- the operations decide() performed in
+ * round 2, in the same order */
+template <int EST>
+VPT_DEV void eqa_medium(const DevScene* __restrict__ S, const Path& p, const Event& e, double sigma_t, double& dist,
+                        double& pdf)
+{
+    const double t = e.t, x = vm_fabs(e.pdf);
+    const bool hit = !__builtin_signbit(e.pdf);
+    const double psurf = EST == 1 ? lm_exp(sigma_t * t * -1.0)
+                                  : (hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0);
+    double D = 0, ta = 0, tb = 0, sd = 0;
+    dist = equiangular_setup(S, e.src, t, p.o, p.d, x, D, ta, tb, sd);
+    pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
+}
+
 template <int EST, bool COUNT, int LT = -1>
-VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
+VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e0,
                           const Medium& m)
 {
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
     const double continueprob = 0.6;
+    Event e = e0;
+    if (VPT_EQA_DEFER && (EST == 1 || EST == 4)) eqa_medium<EST>(S, p, e0, sigma_t, e.dist, e.pdf);
     dv3 xt = add(p.o, scl(p.d, e.dist));
     if (EST == 3) {  /* implicit: vptShadeMethods.h:1000-1006 */
         const double T = transmitance(p.o, xt, sigma_t);

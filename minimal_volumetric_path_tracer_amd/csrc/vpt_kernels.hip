@@ -680,7 +680,10 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         HIP_OK(hipGetLastError());
         return slot_done(sl, stream);
     }
+#if VPT_DEBUG_ENV
+    /* the round-1 wave scheduler (render_kernel), an A/B path of debug builds only */
     if constexpr (EST <= 1) return launch_wave<EST, COUNT, FB>(ctx, K, stream);
+#endif
     return VPT_OK;
 }
 

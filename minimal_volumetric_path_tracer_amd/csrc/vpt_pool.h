@@ -65,6 +65,9 @@ namespace vpt {
 #ifndef VPT_RUN_EVENT_ORDER
 #define VPT_RUN_EVENT_ORDER 0  /* 1: the rare surface rings tested first (with VPT_RARE_HINT); 0: index order (A/B 55.71 ms / 269.8) */
 #endif
+#ifndef VPT_SCHED_FAST
+#define VPT_SCHED_FAST 0    /* 1: scheduler with one counter read per batch and ring bases by v_readlane (A/B 51.48 -> 51.65 ms FF: no gain) */
+#endif
 #ifndef VPT_MERGE_LIGHTS
 #define VPT_MERGE_LIGHTS 0  /* bit 0: the diffuse surface rings' code shared by both light kinds; bit 1: the medium rings' */
 #endif
@@ -88,9 +91,9 @@ constexpr int NF = 18;      /* doubles per task */
 constexpr int NR = 7;       /* rings */
 constexpr int R_A = 0, R_S = 1, R_M = 5, R_DONE = NR;
 /* the scheduler's counters (TaskPool::ctl): ring tails, ring heads, slots retired, the unit ring's
- * tail, queue exhausted, refill in progress */
+ * tail, queue exhausted, refill in progress, the unit ring's head (one lane-parallel read fetches all) */
 constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_EXH = 2 * NR + 2, C_RFL = 2 * NR + 3,
-              NCTL = 2 * NR + 4;
+              C_UHEAD = 2 * NR + 4, NCTL = 2 * NR + 5;
 static_assert(NCTL <= 64, "the counters are read lane-parallel by one wave");
 #ifndef VPT_UREFILL
 #define VPT_UREFILL 128
@@ -134,8 +137,7 @@ struct TaskPool {
      * monotonic ring tails and heads, slots retired, the unit ring's tail, queue exhausted */
     int ctl[NCTL];
     int ticket, serving;     /* FIFO ticket lock: a wave returning tasks is never starved */
-    uint32_t uring[URING];   /* prefetched work units (refilled under the lock, taken by CAS on uhead) */
-    int uhead;
+    uint32_t uring[URING];   /* prefetched work units (refilled under the lock, taken by CAS on ctl[C_UHEAD]) */
 };
 
 /* Lock-free rings (VPT_LOCKFREE): an entry is the slot and the lap of its ring position,
@@ -415,7 +417,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             while (true) {
                 if (lane == leader) {
                     ex = __hip_atomic_load(&sh.ctl[C_EXH], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    h = lds_peek(&sh.uhead);
+                    h = lds_peek(&sh.ctl[C_UHEAD]);
                     const int avail =
                         __hip_atomic_load(&sh.ctl[C_UTAIL], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - h;
                     got = max(0, min(k, avail));
@@ -440,7 +442,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                 int won = 0;
                 if (lane == leader) {
                     int hh = h;
-                    won = __hip_atomic_compare_exchange_strong(&sh.uhead, &hh, h + got, __ATOMIC_RELAXED,
+                    won = __hip_atomic_compare_exchange_strong(&sh.ctl[C_UHEAD], &hh, h + got, __ATOMIC_RELAXED,
                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 if (__builtin_amdgcn_readlane(won, leader)) break;
@@ -546,7 +548,9 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             result = R_S + (sk == 0 ? (EST == 3 || EST == 5 ? 0 : S->geo[t.e.src].point) : sk);
         } else {
             result = R_M + (EST == 3 ? 0 : S->geo[t.e.src].point);
-            t.e.t = t.e.dist;  /* one slot (F_TD): stage M reads the sampled distance */
+            /* one slot (F_TD): stage M reads the sampled distance -- or, for the deferred
+             * equi-angular estimators, tMax (with the draw in F_PDF) */
+            if (!(VPT_EQA_DEFER && (EST == 1 || EST == 4))) t.e.t = t.e.dist;
         }
         SECT_END(dci, SECT_A_DECIDE_IN);
     }
@@ -575,7 +579,6 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
     if (tid < NCTL) sh.ctl[tid] = tid == C_TAIL + R_A ? POOL : 0;  /* every slot starts in ring A */
     if (tid == 0) {
         sh.ticket = sh.serving = 0;
-        sh.uhead = 0;
     }
     sect_init();
     __syncthreads();
@@ -610,7 +613,18 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             int base = 0;
             if (lane < NR && cnt > 0)
                 base = __hip_atomic_fetch_add(&sh.ctl[C_TAIL + lane], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if VPT_SCHED_FAST
+            /* each lane's ring base from the lane that reserved it: v_readlane, not an LDS permute */
+            int bsel = 0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int br = __builtin_amdgcn_readlane(base, r);
+                bsel = next == r ? br : bsel;
+            }
+            const int pos = bsel + rank;
+#else
             const int pos = __shfl(base, ret ? next : 0) + rank;
+#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  /* task states before their entries */
             if (ret) ((volatile uint16_t*)sh.ring[next])[pos % POOL] = ring_entry(slot, pos);
             const uint64_t md = __ballot(lane < n && next == R_DONE);
@@ -619,14 +633,17 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         }
         /* keep the unit ring stocked (the queue atomic's latency is paid once per 128 units); one
          * wave at a time, claimed by a flag */
+        int v0 = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;  /* reused by the claim below (VPT_SCHED_FAST) */
+        bool reread = !VPT_SCHED_FAST;
         {
-            const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+            const int v = v0;
             if (dbg && !seen_exh && __builtin_amdgcn_readlane(v, C_EXH)) {
                 seen_exh = true;
                 if (lane == 0) dbg_tl(stats, 1, false);
             }
             if (VPT_UNLIKELY(!__builtin_amdgcn_readlane(v, C_EXH) && !__builtin_amdgcn_readlane(v, C_RFL) &&
-                __builtin_amdgcn_readlane(v, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL)) {
+                __builtin_amdgcn_readlane(v, C_UTAIL) - __builtin_amdgcn_readlane(v, C_UHEAD) < UREFILL)) {
+                reread = true;
                 int own = 0;
                 if (lane == 0) {
                     int z = 0;
@@ -635,7 +652,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                 }
                 if (__builtin_amdgcn_readfirstlane(own)) {
                     const int t0 = __builtin_amdgcn_readfirstlane(lds_peek(&sh.ctl[C_UTAIL]));
-                    if (t0 - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL) {
+                    if (t0 - __builtin_amdgcn_readfirstlane(lds_peek(&sh.ctl[C_UHEAD])) < UREFILL) {
                         unsigned ubase = 0;
                         if (lane == 0) ubase = atomicAdd(P.queue, (unsigned)UREFILL);
                         ubase = (unsigned)__builtin_amdgcn_readfirstlane((int)ubase);
@@ -658,7 +675,8 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         int st = 0, take = 0;
         bool fin = false;
         while (true) {
-            const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+            const int v = reread ? (lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0) : v0;
+            reread = true;
             int best = 0;
             st = 0;
 #pragma unroll
@@ -770,7 +788,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         /* keep the unit ring stocked: the queue atomic's latency is paid here once per 128 units
          * instead of in every stage-A round (all waves on the chip contend for that address) */
         if (!__builtin_amdgcn_readlane(cv, C_EXH) &&
-            __builtin_amdgcn_readlane(cv, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.uhead)) < UREFILL) {
+            __builtin_amdgcn_readlane(cv, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.ctl[C_UHEAD])) < UREFILL) {
             unsigned base = 0;
             if (lane == 0) base = atomicAdd(P.queue, (unsigned)UREFILL);
             base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
