@@ -627,6 +627,29 @@ VPT_DEV dv3 refrax_dielectric(double etai, double etat, dv3 wi, dv3 n)
 }
 
 /* ------------------------------------------------------------------ shading records */
+/* per-sphere flag of a per-lane sphere index: a shift of a wave-uniform mask (DevScene m_*) instead of
+ * a per-lane load of the GeoSphere record (whose latency sat on decide()'s critical path) */
+VPT_DEV int sph_flag(uint64_t m, int i) { return (int)((m >> (i & 63)) & 1ull); }
+
+/* the emitter list's entry j (vptShadeMethods.h:1293-1303, idsource = arr[rand * count]): up to 8
+ * emitters by selects over scalar loads, else a per-lane load */
+#ifndef VPT_EMIT_SELECT
+#define VPT_EMIT_SELECT 0  /* 1: selects over scalar loads for <= 8 emitters (A/B 50.58 -> 51.20 ms FF, 222.9 -> 226.9 MIS: slower) */
+#endif
+VPT_DEV int emit_pick(const DevScene* __restrict__ S, int j, int count)
+{
+#if VPT_EMIT_SELECT
+    if (count <= 8) {
+        int src = S->emit[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k)
+            if (k < count) src = j == k ? S->emit[k] : src;
+        return src;
+    }
+#endif
+    return S->emit[j];
+}
+
 VPT_DEV dv3 sph_c(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].c); }
 VPT_DEV dv3 sph_rad(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].radiance); }
 VPT_DEV dv3 sph_p(const DevScene* __restrict__ S, int i) { return ld3(S->sph[i].p); }
@@ -856,6 +879,7 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     int lt[2];
     dv3 dirs[3];
     double cm[2], xtra[2] = {0, 0};
+    dv3 cxk[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         lt[k] = S->mis_light[k];
@@ -864,8 +888,25 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         cx = scl(cx, (1 / normcx));
         const double lr = S->sph[lt[k]].r;
         cm[k] = vm_sqrt(1 - (lr / normcx) * (lr / normcx));
-        dirs[k] = solid_angle_dir(smp, cx, cm[k]);
-        if (omat == 2) xtra[k] = smp.next();  /* the dielectric pdf coin of the light loop */
+        cxk[k] = cx;
+    }
+    if (omat != 2) {  /* both cone samples' draws (e0, phi per light, samplingFunctions.h:65-82), then their trig together */
+        const double e00 = smp.next();
+        const double c0 = (1 - e00) + e00 * cm[0];
+        const double phi0 = 2 * VPT_PI * smp.next();
+        const double e01 = smp.next();
+        const double c1 = (1 - e01) + e01 * cm[1];
+        const double phi1 = 2 * VPT_PI * smp.next();
+        double st0, ct0, sp0, cp0, st1, ct1, sp1, cp1;
+        lm_dir_trig2(c0, phi0, c1, phi1, &st0, &ct0, &sp0, &cp0, &st1, &ct1, &sp1, &cp1);
+        dirs[0] = nrm(from_local(cxk[0], st0 * cp0, st0 * sp0, ct0));
+        dirs[1] = nrm(from_local(cxk[1], st1 * cp1, st1 * sp1, ct1));
+    } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            dirs[k] = solid_angle_dir(smp, cxk[k], cm[k]);
+            xtra[k] = smp.next();  /* the dielectric pdf coin of the light loop */
+        }
     }
     dv3 wt_s = mk(0, 0, 0), wh_m = mk(0, 0, 0), wo_l = mk(0, 0, 0), wi_m = mk(0, 0, 0);
     bool refl = false;
@@ -1019,7 +1060,7 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
     const dv3 I = sph_rad(S, src);
     const dv3 light = sph_p(S, src);
     const double lr = PT == 1 ? 0.0 : S->sph[src].r;
-    const bool l3 = S->geo[src].mat3;
+    const bool l3 = sph_flag(S->m_mat3, src);
     dv3 Le;
     if (visibility(S, smp, light, x, false, lr, l3)) {
         Le = scl(I, (1 / (dot(sub(light, x), sub(light, x)))));
@@ -1231,7 +1272,7 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
         e.dist = -lm_log(1 - smp.next()) / sigma_t;
         e.pdf = (sigma_t * lm_exp(sigma_t * e.dist * -1.0)) * (1.0 - TrActual);  /* :977 */
         if (!(e.dist > t)) return EV_MED;
-        if (S->geo[id].emitter) {  /* :978-980: a light returns its radiance at any depth */
+        if (sph_flag(S->m_emitter, id)) {  /* :978-980: a light returns its radiance at any depth */
             p.L = add(p.L, mul(p.beta, sph_rad(S, id)));
             return EV_END;
         }
@@ -1239,7 +1280,7 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
     }
     const int count = S->n_emit;
     if (VPT_UNLIKELY(count == 0)) return EV_END;
-    e.src = S->emit[(int)(smp.next() * count)];
+    e.src = emit_pick(S, (int)(smp.next() * count), count);
     bool surf;
     if (est_free_flight<EST>()) {
         e.dist = -lm_log(1 - smp.next()) / sigma_t;  /* freeFlightSample, vptSamplingFunctions.h:11-14 */
@@ -1259,7 +1300,7 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
         surf = EST == 1 ? smp.next() < psurf : smp.next() <= psurf;  /* :1423 / :1096 */
     }
     if (!surf) return EV_MED;
-    if (S->geo[id].emitter) {  /* the path ends on a light; only a camera ray sees it */
+    if (sph_flag(S->m_emitter, id)) {  /* the path ends on a light; only a camera ray sees it */
         if (p.depth == 0) p.L = EST == 0 ? mul(sph_rad(S, id), p.beta) : sph_rad(S, id);
         return EV_END;
     }
@@ -1508,7 +1549,7 @@ __device__ static dv3 trace_ray_marching(const DevScene* __restrict__ S, Sampler
     dv3 Li = mk(0, 0, 0);
     const dv3 lp = sph_p(S, src);
     const double lr = S->sph[src].r;
-    const bool l3 = S->geo[src].mat3;
+    const bool l3 = sph_flag(S->m_mat3, src);
     const double steps = t / step;
     if (!(steps < (double)VPT_MARCH_MAX_STEPS)) return mk(__builtin_nan(""), __builtin_nan(""), __builtin_nan(""));
     for (int i = 0; i < steps; i++) {

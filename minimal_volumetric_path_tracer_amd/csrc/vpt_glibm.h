@@ -266,6 +266,10 @@ VM_TABLE(gm_acos_tab, {
     0x1.921fb54442d18p+0, 0x1.1a62633145c07p-54, 0x1.921fb54442d18p+1})  /* 11-13 hp0, hp1, pi */
 enum { GA_F6 = 0, GA_RT3 = 6, GA_T27 = 10, GA_HP0, GA_HP1, GA_PI };
 
+/* gm_acos outside glibc's table range (|x| < 0.125, |x| >= 0.96875, NaN): straight-line, every
+ * such argument (the cone samplers' cosines are all > 0.9925) */
+VM_QUAL double gm_acos_bc(double x);
+
 VM_QUAL double gm_acos(double x)
 {
     vm_ct* K = vm_tab(gm_acos_tab);
@@ -291,6 +295,19 @@ VM_QUAL double gm_acos(double x)
         const double y = T[d + 2];
         res = m > 0 ? (HP1 - t) + (HP0 - y) : (t + HP1) + (y + HP0);
     } else {
+        res = gm_acos_bc(x);
+    }
+    return res;
+}
+
+VM_QUAL double gm_acos_bc(double x)
+{
+    vm_ct* K = vm_tab(gm_acos_tab);
+    const double HP0 = VM_T(K, GA_HP0), HP1 = VM_T(K, GA_HP1);
+    const int32_t m = gm_hi(x);
+    const uint32_t k = (uint32_t)m & 0x7fffffffu;
+    double res;
+    {
         /* 0.96875 <= |x| < 1 (B): acos = 2 asin(sqrt(z)) or pi - that, z = (1 - |x|)/2;
          * |x| < 0.125 (C; hp0 for |x| < 2^-55); |x| = 1; |x| > 1 and NaN.  B and C evaluate the same
          * odd asin polynomial (in z, in x^2): one path, one Horner loop, the result selected (a
@@ -547,8 +564,26 @@ GM_CALLQ gm_sc2 gm_sincos_acos_phi_cone(double c, double phi)
 {
     vm_ct* K = vm_tab(gm_sc_tab);
     gm_sc2 r;
-    gm_sincos_fused_r(K, gm_acos(c), &r.s0, &r.c0, 1, 1);
+    gm_sincos_fused_r(K, gm_acos_bc(c), &r.s0, &r.c0, 1, 1);  /* c > 0.9925: acos outside the table range */
     gm_sincos_k(K, phi, &r.s1, &r.c1);
+    return r;
+}
+
+/* two cone directions at once (MISv2's two light samples, include/samplingFunctions.h:163-206): the
+ * same evaluations as two gm_sincos_acos_phi_cone calls, straight-line, so that the two independent
+ * chains (and their table reads) overlap */
+typedef struct {
+    gm_sc2 a, b;
+} gm_sc4;
+GM_CALLQ gm_sc4 gm_sincos_acos_phi_cone2(double c0, double phi0, double c1, double phi1)
+{
+    vm_ct* K = vm_tab(gm_sc_tab);
+    gm_sc4 r;
+    const double t0 = gm_acos_bc(c0), t1 = gm_acos_bc(c1);
+    gm_sincos_fused_r(K, t0, &r.a.s0, &r.a.c0, 1, 1);
+    gm_sincos_fused_r(K, t1, &r.b.s0, &r.b.c0, 1, 1);
+    gm_sincos_k(K, phi0, &r.a.s1, &r.a.c1);
+    gm_sincos_k(K, phi1, &r.b.s1, &r.b.c1);
     return r;
 }
 

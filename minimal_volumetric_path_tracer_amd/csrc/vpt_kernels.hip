@@ -810,6 +810,12 @@ int vpt_set_scene(vpt_context* ctx, const vpt_sphere* s, int n)
         h.geo[i].skey = q.material == 0 ? 0 : q.material == 1 ? 2 : 3;
         h.geo[i].point = q.r == 0;
         if (h.geo[i].emitter) h.emit[h.n_emit++] = i;
+        const uint64_t bit = 1ull << i;
+        if (h.geo[i].emitter) h.m_emitter |= bit;
+        if (h.geo[i].point) h.m_point |= bit;
+        if (h.geo[i].mat3) h.m_mat3 |= bit;
+        if (h.geo[i].skey & 1) h.m_skey1 |= bit;
+        if (h.geo[i].skey & 2) h.m_skey2 |= bit;
         if (q.r > 0 && q.radiance[0] > 0) h.mis_light[h.n_mis++] = i;
         if (q.material == 3) h.n_mat3++;
     }

@@ -544,10 +544,10 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             t.in_path = false;
             result = R_A;
         } else if (ev == EV_SURF) {  /* (the implicit estimator, EST 3, picks no light) */
-            const int sk = S->geo[t.e.id].skey;
-            result = R_S + (sk == 0 ? (EST == 3 || EST == 5 ? 0 : S->geo[t.e.src].point) : sk);
+            const int sk = sph_flag(S->m_skey1, t.e.id) | (sph_flag(S->m_skey2, t.e.id) << 1);
+            result = R_S + (sk == 0 ? (EST == 3 || EST == 5 ? 0 : sph_flag(S->m_point, t.e.src)) : sk);
         } else {
-            result = R_M + (EST == 3 ? 0 : S->geo[t.e.src].point);
+            result = R_M + (EST == 3 ? 0 : sph_flag(S->m_point, t.e.src));
             /* one slot (F_TD): stage M reads the sampled distance -- or, for the deferred
              * equi-angular estimators, tMax (with the draw in F_PDF) */
             if (!(VPT_EQA_DEFER && (EST == 1 || EST == 4))) t.e.t = t.e.dist;
