@@ -50,10 +50,13 @@ VPT_CK vpt_chunk_layout vpt_chunks(int spp, int C, int taper)
 /* auto chunk size (vpt_params.chunk_spp == 0): 32 samples (A/B at 1024^2 x 256 spp), more
  * above 4096 spp so that a pixel has at most 128 chunks + the taper (4096^2 x 8192 spp on one GPU:
  * 2.3e9 work units < 2^32, 55 GB of partials); spp <= 32 is one chunk */
+#ifndef VPT_AUTO_CHUNK_MIN
+#define VPT_AUTO_CHUNK_MIN 32
+#endif
 VPT_CK int vpt_auto_chunk(int spp)
 {
     int c = (spp + 127) / 128;
-    if (c < 32) c = 32;
+    if (c < VPT_AUTO_CHUNK_MIN) c = VPT_AUTO_CHUNK_MIN;
     return c < spp ? c : spp;
 }
 

@@ -439,6 +439,9 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
 }
 
 /* ------------------------------------------------------------------ sampling */
+#ifndef VPT_POINT_CONE
+#define VPT_POINT_CONE 1  /* dir_from_cos: the cone toward a point light without its trig and frame (exact) */
+#endif
 /* direction at polar angle theta = acos(c) and azimuth phi around n: the reference computes
  * sin(acos c), cos(acos c), sin(phi), cos(phi) with libm (lm_dir_trig, bit for bit) */
 VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
@@ -450,6 +453,11 @@ VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
          * the azimuth's sin and cos are evaluated -- the same bits */
         st = 0.0;
         ct = 1.0;
+        /* ... and when no component of n is zero, not even those: from_local(n, 0 cp, 0 sp, 1) =
+         * (s (+-0) + t (+-0)) + n 1 = n exactly (the frame of a unit n is finite, so s and t scale
+         * to signed zeros, which a nonzero n_k absorbs) -- the azimuth draw is taken by the caller */
+        if (VPT_POINT_CONE && __ballot(n.x == 0 || n.y == 0 || n.z == 0 || !(n.x - n.x == 0 && n.y - n.y == 0 && n.z - n.z == 0)) == 0)
+            return nrm(n);
         lm_sincos(phi, &sp, &cp);
     } else {
         lm_dir_trig(c, phi, &st, &ct, &sp, &cp);
