@@ -439,6 +439,9 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
 }
 
 /* ------------------------------------------------------------------ sampling */
+#ifndef VPT_POINT_H5
+#define VPT_POINT_H5 1    /* single_scattering: a point light's cone hit scores +-0 without computing it */
+#endif
 #ifndef VPT_POINT_CONE
 #define VPT_POINT_CONE 1  /* dir_from_cos: the cone toward a point light without its trig and frame (exact) */
 #endif
@@ -1105,7 +1108,8 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
  * point-light medium events (counting mode still adds its tests). */
 template <bool COUNT, int LT = -1>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
 VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
-                              double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource)
+                              double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource,
+                              bool zero_ok = false)
 {
     const double lr = LT == 1 ? 0.0 : S->sph[src].r;
     const dv3 lp = sph_p(S, src);
@@ -1130,11 +1134,16 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     SECT_BEGIN(sw);
     if (src == idHit) {
         if (point) smp.tests(S->n);  /* the shadow ray the reference casts first (result overwritten) */
-        double it = lm_exp(sigma_t * tdist * -1.0);
-        double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, wl);
-        dv3 Ls = scl(scl(rad, it), ph);
-        if (with_sigma) Ld = scl(scl(scl(scl(Ls, trxt), sigma_s), (1 / prob_wl)), (1 / probSource));
-        else Ld = scl(scl(Ls, (1 / prob_wl)), (1 / probSource));
+        /* a point light's cone (cmax == 1: prob_wl = +inf) scores Ls * (1 / inf) = +-0 with Ls finite
+         * (SURVEY H5); zero_ok: the caller's update absorbs a signed zero (finite throughput and
+         * pdf), so +0 is the same result without the exponential and the phase value */
+        if (!(LT == 1 && VPT_POINT_H5 && zero_ok && cmax == 1.0)) {
+            double it = lm_exp(sigma_t * tdist * -1.0);
+            double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, wl);
+            dv3 Ls = scl(scl(rad, it), ph);
+            if (with_sigma) Ld = scl(scl(scl(scl(Ls, trxt), sigma_s), (1 / prob_wl)), (1 / probSource));
+            else Ld = scl(scl(Ls, (1 / prob_wl)), (1 / probSource));
+        }
     } else if (point) {
         SECT_BEGIN(swi);
         if (visibility(S, smp, lp, xt, false, -1.0, false)) {
@@ -1458,9 +1467,13 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
         return;
     }
     const double probSource = 1.0 / S->n_emit;
+    /* the updates below absorb a +-0 Ld exactly when the throughput (and, equi-angular, 1 / pdf) is
+     * finite (p.L is never -0: it starts at +0 and only adds) -- single_scattering's H5 shortcut */
+    const bool zero_ok = p.beta.x - p.beta.x == 0 && p.beta.y - p.beta.y == 0 && p.beta.z - p.beta.z == 0 &&
+                         (!(EST == 1 || EST == 4) || (1 / e.pdf) - (1 / e.pdf) == 0);
     if (EST == 0) {
         SECT_BEGIN(ss);
-        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
+        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource, zero_ok);
         SECT_END(ss, SECT_M_SS);
         SECT_BEGIN(ph);
         dv3 wi = phase_sample(smp, p.d);
@@ -1469,7 +1482,7 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else if (EST == 2) {  /* vptShadeMethods.h:1252-1258 */
-        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource);
+        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource, zero_ok);
         dv3 wi = phase_sample(smp, p.d);
         p.L = add(p.L, mul(p.beta, scl(scl(Ld, (sigma_s / sigma_t)), (1 / continueprob))));
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
@@ -1477,7 +1490,7 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
     } else {
         double T = transmitance(p.o, xt, sigma_t);
         SECT_BEGIN(ss);
-        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, true, sigma_s, T, probSource);
+        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, true, sigma_s, T, probSource, zero_ok);
         SECT_END(ss, SECT_M_SS);
         SECT_BEGIN(ph);
         dv3 wi = phase_sample(smp, p.d);
