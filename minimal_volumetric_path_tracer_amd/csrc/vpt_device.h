@@ -91,7 +91,8 @@ namespace vpt {
 enum {
     SECT_SCHED = 0, SECT_LOAD, SECT_S_PLIGHT, SECT_S_MIS, SECT_S_MIS_ISECT, SECT_S_BDSF, SECT_M_SS, SECT_M_SS_DIR,
     SECT_M_SS_ISECT, SECT_M_SS_SHADOW, SECT_M_PHASE, SECT_CONT, SECT_A_PREP, SECT_A_DECIDE, SECT_A_ISECT, SECT_STORE,
-    SECT_S_TOTAL, SECT_M_TOTAL, SECT_A_CAMERA, SECT_A_DECIDE_IN, SECT_M_SHADOW_IN, SECT_A_CAMERA_IN, SECT_USED,
+    SECT_S_TOTAL, SECT_M_TOTAL, SECT_A_CAMERA, SECT_A_DECIDE_IN, SECT_M_SHADOW_IN, SECT_A_CAMERA_IN, SECT_M_EQA,
+    SECT_M_TR, SECT_USED,
     SECT_N = 32
 };
 #if VPT_SECTIONS
@@ -130,14 +131,13 @@ __device__ static inline __attribute__((always_inline)) void sect_add(int k, uin
 __device__ static inline __attribute__((always_inline)) void sect_init()
 {
 #if VPT_SECTIONS
-    if ((threadIdx.x & 63) < 3 * SECT_USED) sect_lds()[threadIdx.x & 63] = 0;
+    for (int l = threadIdx.x & 63; l < 3 * SECT_USED; l += 64) sect_lds()[l] = 0;
 #endif
 }
 __device__ static inline __attribute__((always_inline)) void sect_flush()
 {
 #if VPT_SECTIONS
-    const int l = threadIdx.x & 63;
-    if (l < 3 * SECT_USED) {
+    for (int l = threadIdx.x & 63; l < 3 * SECT_USED; l += 64) {
         const uint32_t v = sect_lds()[l];
         atomicAdd(&g_vpt_sect[l < SECT_USED ? l : l < 2 * SECT_USED ? SECT_N + l - SECT_USED : 2 * SECT_N + l - 2 * SECT_USED],
                   (unsigned long long)v);
@@ -303,6 +303,57 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
     return 0;
 }
 
+/* scene_intersect_grouped for rays that all leave one point o, with oc = o - centre and
+ * |oc|^2 of every sphere taken from oc[i][0..3] (formed once by the caller with the same operations,
+ * march_origin_init): per sphere only b and det are formed -- the same values, the same result */
+template <int G, bool COUNT>
+VPT_DEV int scene_intersect_grouped_oc(const DevScene* __restrict__ S, Sampler<COUNT>& smp, const double (*oc)[4],
+                                       dv3 d, double& t, int& id)
+{
+    double tmin = VPT_DBL_MAX;
+    int contact = 0;
+    const int n = S->n;
+    int i = 0;
+    for (; i + G <= n; i += G) {
+        double b[G], det[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const double ocx = oc[i + k][0], ocy = oc[i + k][1], ocz = oc[i + k][2], cc = oc[i + k][3];
+            b[k] = ocx * d.x + ocy * d.y + ocz * d.z;
+            det[k] = b[k] * b[k] - cc + S->geo[i + k].r2;
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) sphere_take(sphere_tact(b[k], det[k]), i + k, tmin, id, contact);
+    }
+    for (; i < n; ++i) {
+        const double ocx = oc[i][0], ocy = oc[i][1], ocz = oc[i][2], cc = oc[i][3];
+        const double b = ocx * d.x + ocy * d.y + ocz * d.z;
+        const double det = b * b - cc + S->geo[i].r2;
+        sphere_take(sphere_tact(b, det), i, tmin, id, contact);
+    }
+    smp.tests(n);
+    if (contact) {
+        t = tmin;
+        return 1;
+    }
+    t = 0;
+    return 0;
+}
+
+/* oc[i] = (o - centre_i, |o - centre_i|^2) for every sphere, by the threads of a workgroup (the
+ * operations of scene_intersect_grouped's first loop) */
+__device__ static inline void march_origin_init(const DevScene* __restrict__ S, dv3 o, double (*oc)[4])
+{
+    for (int i = (int)threadIdx.x; i < S->n; i += (int)blockDim.x) {
+        const GeoSphere g = S->geo[i];
+        const double ocx = o.x - g.px, ocy = o.y - g.py, ocz = o.z - g.pz;
+        oc[i][0] = ocx;
+        oc[i][1] = ocy;
+        oc[i][2] = ocz;
+        oc[i][3] = ocx * ocx + ocy * ocy + ocz * ocz;
+    }
+}
+
 /* every intersection site (not only decide) through the grouped loop (A/B knob) */
 #ifndef VPT_ISECT_GROUP_ALL
 #define VPT_ISECT_GROUP_ALL 5
@@ -361,7 +412,7 @@ VPT_DEV int scene_isect(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3
  * light point is a sphere centre (exact shortcut, header comment), negative otherwise. */
 template <bool COUNT>
 VPT_DEV int visibility(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 light, dv3 x, bool skip3,
-                       double light_r, bool light_is3)
+                       double light_r, bool light_is3, const double (*light_oc)[4] = nullptr)
 {
     dv3 lx = sub(light, x);
     double distance = vm_sqrt(dot(lx, lx));
@@ -373,7 +424,8 @@ VPT_DEV int visibility(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 
     lx = scl(lx, -1);
     int id = 0;
     double t;
-    scene_isect(S, smp, light, lx, t, id, skip3);
+    if (light_oc != nullptr && !skip3) scene_intersect_grouped_oc<VPT_ISECT_GROUP_ALL>(S, smp, light_oc, lx, t, id);
+    else scene_isect(S, smp, light, lx, t, id, skip3);
     return (t > distance || t == 0);
 }
 
@@ -1455,7 +1507,9 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
     const double sigma_t = sigma_a + sigma_s;
     const double continueprob = 0.6;
     Event e = e0;
+    SECT_BEGIN(eq);
     if (VPT_EQA_DEFER && (EST == 1 || EST == 4)) eqa_medium<EST>(S, p, e0, sigma_t, e.dist, e.pdf);
+    SECT_END(eq, SECT_M_EQA);
     dv3 xt = add(p.o, scl(p.d, e.dist));
     if (EST == 3) {  /* implicit: vptShadeMethods.h:1000-1006 */
         const double T = transmitance(p.o, xt, sigma_t);
@@ -1488,7 +1542,9 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else {
+        SECT_BEGIN(tr);
         double T = transmitance(p.o, xt, sigma_t);
+        SECT_END(tr, SECT_M_TR);
         SECT_BEGIN(ss);
         dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, true, sigma_s, T, probSource, zero_ok);
         SECT_END(ss, SECT_M_SS);
@@ -1559,7 +1615,7 @@ __device__ static dv3 trace_surface_pt(const DevScene* __restrict__ S, Sampler<C
 #endif
 template <bool COUNT>
 __device__ static dv3 trace_ray_marching(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d,
-                                         const Medium& m)
+                                         const Medium& m, const double (*light_oc)[4] = nullptr)
 {
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s, step = m.march_step;
     const int src = m.march_light;
@@ -1580,7 +1636,7 @@ __device__ static dv3 trace_ray_marching(const DevScene* __restrict__ S, Sampler
         const double phase = 1 / (4 * VPT_PI);  /* isotropicPhaseFunction, volumetricBasicFunctions.h:59-62 */
         const dv3 wc = sub(lp, xt);
         const double normwc = dot(wc, wc);
-        if (visibility(S, smp, lp, xt, false, lr, l3)) {
+        if (visibility(S, smp, lp, xt, false, lr, l3, light_oc)) {
             const dv3 Le = scl(sph_rad(S, src), (1 / normwc));
             const dv3 Ls = scl(Le, (phase * transmitance(xt, lp, sigma_a + sigma_s)));
             Li = add(Li, scl(scl(scl(Ls, T), sigma_s), step));
@@ -1733,12 +1789,13 @@ VPT_DEV dv3 punctual_volumetric(const DevScene* __restrict__ S, Sampler<COUNT>& 
 
 /* One camera sample, sequentially (the reference's per-sample call; used by vpt_trace_batch). */
 template <int EST, bool COUNT>
-__device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, const Medium& m)
+__device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, const Medium& m,
+                                  const double (*march_oc)[4] = nullptr)
 {
     if constexpr (EST == 5) {
         return trace_surface_pt<COUNT>(S, smp, o, d);
     } else if constexpr (EST == 6) {
-        return trace_ray_marching<COUNT>(S, smp, o, d, m);
+        return trace_ray_marching<COUNT>(S, smp, o, d, m, march_oc);
     } else if constexpr (EST == 7) {
         return trace_ray_marching2<COUNT>(S, smp, o, d, m);
     } else if constexpr (EST == 8) {

@@ -50,12 +50,22 @@ struct KParams {
             return vpt_fail(VPT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));       \
     } while (0)
 
+#ifndef VPT_MARCH_OC
+#define VPT_MARCH_OC 1
+#endif
 template <int EST, bool COUNT, int FB>
 __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const DevScene* __restrict__ S)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    /* rayMarching3: every shadow ray leaves the light's centre, so oc and |oc|^2 of each sphere are
+     * formed once per workgroup (VPT_MARCH_OC) */
+    __shared__ double march_oc[EST == 6 && VPT_MARCH_OC ? VPT_MAX_SPHERES : 1][4];
+    if (EST == 6 && VPT_MARCH_OC) {
+        march_origin_init(S, sph_p(S, P.march_light), march_oc);
+        __syncthreads();
+    }
     if (x >= P.w || lr >= P.shard_rows) return;
     const int k = lr / P.band_rows, r = lr - k * P.band_rows;
     const int fr = (P.band_offset + k * P.band_stride) * P.band_rows + r;  /* file row */
@@ -77,7 +87,7 @@ __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const Dev
         double jy = smp.next();
         dv3 dir = add(add(scl(cx, (((double)x + jx - 0.5) / P.w - .5)), scl(cy, (((double)y + jy - 0.5) / P.h - .5))), cd);
         dir = nrm(dir);
-        dv3 L = trace_sample<EST, COUNT>(S, smp, o, dir, m);
+        dv3 L = trace_sample<EST, COUNT>(S, smp, o, dir, m, EST == 6 && VPT_MARCH_OC ? march_oc : nullptr);
         acc = add(L, acc);
         if (COUNT) {
             tests += smp.cnt.tests;
