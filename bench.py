@@ -166,6 +166,37 @@ def run_reference_program(exe: str, spp: int, cpus: list) -> float:
     return float(m.group(1))
 
 
+def reference_estimator_rate(est: int, c: dict, cpus: list, rows_per: int = 4, spp: int = 256) -> dict:
+    """The reference's own estimator `est` (oracle/_ref/libvpt_ref.so) on len(cpus) cores at once: one
+    process per core (oracle/ref_rate.py; the harness drives the reference's global erand48 state),
+    each pinned to its core and rendering `rows_per` file rows x width x `spp` samples of the image.
+    Rate = all samples / the longest child's render time (the children start within milliseconds
+    of each other; their interpreter start-up is outside the timed renders)."""
+    H, W = c["height"], c["width"]
+    saved = os.sched_getaffinity(0)
+    procs = []
+    try:
+        for k, cpu in enumerate(cpus):
+            rows = [(H * (k * rows_per + j)) // (len(cpus) * rows_per) for j in range(rows_per)]
+            os.sched_setaffinity(0, [cpu])
+            procs.append(subprocess.Popen([sys.executable, "-m", "oracle.ref_rate", str(est), str(W), str(H), str(spp),
+                                           repr(c["sigma_a"]), repr(c["sigma_s"])] + [str(r) for r in rows],
+                                          cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                          env=dict(os.environ, OMP_NUM_THREADS="1")))
+    finally:
+        os.sched_setaffinity(0, saved)
+    times = []
+    for p in procs:
+        out, err = p.communicate(timeout=300)
+        if p.returncode != 0:
+            raise RuntimeError(f"oracle.ref_rate rc {p.returncode}: {err[-300:]}")
+        times.append(float(out.strip().splitlines()[-1]))
+    n = len(cpus) * rows_per * W * spp
+    return {"value": n / max(times) / 1e6, "cores": len(cpus),
+            "sample": f"{len(cpus)} processes, one per core, {rows_per} file rows x {W} x {spp} spp each, "
+                      f"renders {min(times):.2f}-{max(times):.2f}s"}
+
+
 def reference_rows_check(img: np.ndarray, c: dict, rows=(0, 1, 2, 3)) -> dict:
     """Per-channel RMSE of the bench image's file rows `rows` (spread over the image) against the
     reference's own functions (oracle/_ref/libvpt_ref.so: the reference headers compiled in place,
@@ -479,21 +510,24 @@ def main() -> None:
             cb = res.get("cpu_baseline")
             if cb:
                 # the reference's own MIS estimator (MISVPTTracerRecursive, isotropic phase: HG is an
-                # extension), one core, on rows of this image; scaled to the socket by the measured
-                # per-thread-flavour parallel efficiency
+                # extension) on rows of this image: measured on the job's cores (one process per core),
+                # then scaled to the socket like the FF figure; the one-core rate beside it
                 from oracle.oracle import Reference  # cpu_baseline leg only
 
                 ref = Reference()
                 ref.set_scene(ref.default_scene())
                 t = time.time()
-                ref.render(cn["width"], cn["height"], 32, 1, cn["sigma_a"], cn["sigma_s"], seed=0x5EED0001, y0=512, y1=514)
-                mis1 = 2 * cn["width"] * 32 / (time.time() - t) / 1e6
-                sock = mis1 * cb["parallel_efficiency"] * cb["socket_physical_cores"]
-                o["cpu_reference"] = {"one_core": mis1, "socket_estimate": sock,
-                                      "how": "reference MISVPTTracerRecursive (oracle/_ref/libvpt_ref.so), 2 rows x "
-                                             f"{cn['width']} x 32 spp on one core, x parallel efficiency "
-                                             f"{cb['parallel_efficiency']:.2f} x {cb['socket_physical_cores']} cores "
-                                             "(an extrapolation from one core: the job has 16 cores, not the socket)",
+                ref.render(cn["width"], cn["height"], 64, 1, cn["sigma_a"], cn["sigma_s"], seed=0x5EED0001, y0=508, y1=516)
+                mis1 = 8 * cn["width"] * 64 / (time.time() - t) / 1e6
+                topo = cpu_topology(threads)
+                misn = reference_estimator_rate(1, cn, topo["cpus"])
+                S = cb["socket_physical_cores"]
+                sock = misn["value"] * S / misn["cores"]
+                o["cpu_reference"] = {"measured": misn, "one_core": mis1, "parallel_efficiency": misn["value"] / (mis1 * misn["cores"]),
+                                      "socket_estimate": sock,
+                                      "how": f"reference MISVPTTracerRecursive (oracle/_ref/libvpt_ref.so) measured on "
+                                             f"{misn['cores']} cores x {S}/{misn['cores']}: an EXTRAPOLATION to the "
+                                             f"{S}-core socket (the job has {misn['cores']} cores, not the socket)",
                                       "phase": "the CPU side runs the reference's ISOTROPIC phase (it has no HG); the "
                                                "GPU side runs HG g=0.5 (the north-star extension, g=0 reduces to "
                                                "the reference bit for bit)"}

@@ -30,3 +30,18 @@ def test_cpu_port_check_rmse():
 def test_bench_configs_match_baseline():
     assert bench.CONFIGS["ff"] == dict(width=1024, height=1024, spp=256, estimator="ff", sigma_a=0.001, sigma_s=0.009)
     assert bench.CONFIGS["mis4k"]["spp"] == 8192 and bench.CONFIGS["mis4k"]["width"] == 4096
+
+
+def test_reference_estimator_rate_multiprocess():
+    """the north-star CPU leg: the reference's MIS estimator in one process per core (oracle/ref_rate.py)"""
+    import os
+    import pytest
+    from oracle.oracle import Reference
+
+    if not Reference.available():
+        pytest.skip("oracle/_ref/libvpt_ref.so not built")
+    cpus = sorted(os.sched_getaffinity(0))[:2]
+    c = dict(width=32, height=16, spp=4, estimator="mis", sigma_a=0.001, sigma_s=0.009)
+    r = bench.reference_estimator_rate(1, c, cpus, rows_per=2, spp=4)
+    assert r["cores"] == len(cpus) and r["value"] > 0
+    assert f"{len(cpus)} processes" in r["sample"]
