@@ -92,7 +92,7 @@ enum {
     SECT_SCHED = 0, SECT_LOAD, SECT_S_PLIGHT, SECT_S_MIS, SECT_S_MIS_ISECT, SECT_S_BDSF, SECT_M_SS, SECT_M_SS_DIR,
     SECT_M_SS_ISECT, SECT_M_SS_SHADOW, SECT_M_PHASE, SECT_CONT, SECT_A_PREP, SECT_A_DECIDE, SECT_A_ISECT, SECT_STORE,
     SECT_S_TOTAL, SECT_M_TOTAL, SECT_A_CAMERA, SECT_A_DECIDE_IN, SECT_M_SHADOW_IN, SECT_A_CAMERA_IN, SECT_M_EQA,
-    SECT_M_TR, SECT_USED,
+    SECT_M_TR, SECT_A_UNIT, SECT_A_R2, SECT_USED,
     SECT_N = 32
 };
 #if VPT_SECTIONS

@@ -81,7 +81,15 @@ namespace vpt {
 #define VPT_PREP_TRIES 2    /* samples a lane may start per preparation round (A/B 1 / 2 / 4 / 8: FF 52.16 / 52.02 / 53.70 / 53.85 ms, MIS 248.1 / 245.2 / 251.9 / 252.0) */
 #endif
 #ifndef VPT_PREP_ROUNDS
-#define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s) */
+#define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; round-2 A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s; round 3: see VPT_PREP_MORE_MIN) */
+#endif
+#ifndef VPT_PREP_MORE_MIN
+/* fewer lanes than this still without a path after a round: parked at once, no further round.  The
+ * second round ran in 99.4 % of batches for ~5 lanes and took 7.1 % of the kernel's wave-time
+ * (profiles/r03/sections_ff_prep.txt).  A/B (kernel ms FF / MIS+HG, profiles/r03/ab_session2.txt):
+ * 0 (always a second round) 49.87 / 222.4; 8 48.46 / 216.1; 16 48.41 / 216.1; 24 48.39 / 215.9;
+ * 32 48.39 / 215.9; one round only (VPT_PREP_ROUNDS=1) 48.11 / 218.1 */
+#define VPT_PREP_MORE_MIN 24
 #endif
 #ifndef VPT_RING_MASK
 #define VPT_RING_MASK 0x7E  /* register-pressure probes only (wrong images otherwise): bit r compiles the S/M code of ring r */
@@ -399,11 +407,14 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
     const unsigned long long c0 = dbg_clock(dbg);
     SECT_BEGIN(pr);
     int round = 0;
+    uint32_t t_r2 = 0;
     while (true) {
         if (dbg) ++D.rounds;
         ++round;
+        if (round == 2) t_r2 = sect_now();
         const bool need = !done && !parked && t.c1 == 0;
         const uint64_t needm = __ballot(need);
+        SECT_BEGIN(un);
         if (needm) {
             const int leader = __ffsll((unsigned long long)needm) - 1;
             const int k = __popcll(needm);
@@ -474,6 +485,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                 }
             }
         }
+        if (needm) SECT_END(un, SECT_A_UNIT);
         if (!done && !parked && !t.in_path && t.c1 != 0) {
             /* up to VPT_PREP_TRIES samples of the unit per round: a sample killed by its first
              * roulette draw costs only its stream start (no LDS, no hand-out), so trying the next
@@ -504,15 +516,19 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                 t.c1 = 0;
             }
         }
-        if (__ballot(!done && !parked && !t.in_path) == 0) break;
+        const uint64_t waiting = __ballot(!done && !parked && !t.in_path);
+        if (waiting == 0) break;
         /* a lane still without a path after VPT_PREP_ROUNDS rounds is parked (back to ring A, it
          * continues from its next sample in a later batch) instead of holding the whole wave in
-         * this loop: the wave's round count is the maximum over its lanes of a geometric count */
-        if (VPT_PREP_ROUNDS > 0 && round >= VPT_PREP_ROUNDS) {
+         * this loop: the wave's round count is the maximum over its lanes of a geometric count.
+         * A further round costs the wave the same whatever its number of lanes, so with fewer than
+         * VPT_PREP_MORE_MIN lanes waiting they are parked at once */
+        if ((VPT_PREP_ROUNDS > 0 && round >= VPT_PREP_ROUNDS) || __popcll(waiting) < VPT_PREP_MORE_MIN) {
             if (!done && !t.in_path) parked = true;
             break;
         }
     }
+    if (round >= 2) sect_add(SECT_A_R2, t_r2);
     SECT_END(pr, SECT_A_PREP);
     SECT_BEGIN(cam);
     if (fresh) {  /* camera ray of the surviving sample: src/rt.cpp:787-789 */

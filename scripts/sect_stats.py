@@ -7,7 +7,7 @@ import minimal_volumetric_path_tracer_amd as vpt
 NAMES = ["sched", "load_task", "S pLight", "S MISv2", "S MISv2 isect3", "S bdsf+update", "M single_scat", "M ss cone dir",
          "M ss cone isect", "M ss shadow/Ld", "M phase", "roulette", "A prep", "A decide", "A decide isect", "store_task",
          "S total", "M total", "A camera", "A decide (in)", "M shadow (in)", "A camera (in)", "M eqa",
-         "M transmittance"]
+         "M transmittance", "A unit handout", "A rounds >= 2"]
 N = 32
 t = vpt.Tracer(0)
 est = sys.argv[1] if len(sys.argv) > 1 else "ff"
