@@ -186,11 +186,17 @@ def reference_estimator_rate(est: int, c: dict, cpus: list, rows_per: int = 4, s
     finally:
         os.sched_setaffinity(0, saved)
     times = []
-    for p in procs:
-        out, err = p.communicate(timeout=300)
-        if p.returncode != 0:
-            raise RuntimeError(f"oracle.ref_rate rc {p.returncode}: {err[-300:]}")
-        times.append(float(out.strip().splitlines()[-1]))
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=300)
+            if p.returncode != 0:
+                raise RuntimeError(f"oracle.ref_rate rc {p.returncode}: {err[-300:]}")
+            times.append(float(out.strip().splitlines()[-1]))
+    finally:  # a timeout or a failed child: the others must not keep pinning cores
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
     n = len(cpus) * rows_per * W * spp
     return {"value": n / max(times) / 1e6, "cores": len(cpus),
             "sample": f"{len(cpus)} processes, one per core, {rows_per} file rows x {W} x {spp} spp each, "

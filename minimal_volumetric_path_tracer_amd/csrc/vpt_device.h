@@ -32,53 +32,23 @@
 #ifndef VPT_ISECT_UNROLL
 #define VPT_ISECT_UNROLL 5
 #endif
-/* rays from the surface point intersected in one pass by MISv2 (0 = off, 2, 3): bit-exact.  Slower
- * before stage A was fused into the S/M wave (off / 2 / 3: 4148 / 4036 / 4063 Ms/s, spills at 256
- * VGPRs), faster since (off / 2 / 3: 5584 / 5569 / 5609) */
-#ifndef VPT_FUSE_RAYS
-#define VPT_FUSE_RAYS 3
-#endif
-#ifndef VPT_FUSE_RARE_MONO
-#define VPT_FUSE_RARE_MONO 1  /* 1: the fused MISv2 only for diffuse surfaces (MK == 0); with VPT_FR_CALL: scratch 448 -> 240 B/lane, L2 reads 267M -> 129M, FF 51.99 -> 51.53 ms */
-#endif
+/* MISv2's three rays from the surface point are intersected in one pass (scene_intersect_n<3>, for
+ * diffuse surfaces): A/B rays fused off / 2 / 3: 5584 / 5569 / 5609 Ms/s (round 2) */
 /* sphere loops taken G spheres at a time (scene_intersect_grouped): decide() and every other
  * site; A/B at 1024^2 x 256: off 4914, decide only G=5 4967 (G=10 4857), all sites G=5 5042, G=3 5009 */
 #ifndef VPT_DECIDE_GROUP
 #define VPT_DECIDE_GROUP 5
 #endif
-/* square roots of the intersection tests computed branch-free (sqrt of max(det, 0), result selected)
- * in the grouped loop (G) and in the fused multi-ray loop (N), so that independent chains overlap */
-#ifndef VPT_BF_G
-#define VPT_BF_G 0
-#endif
-#ifndef VPT_BF_N
-#define VPT_BF_N 0
-#endif
+static_assert(VPT_DECIDE_GROUP >= 1, "spheres are taken G >= 1 at a time");
 
 namespace vpt {
 
 /* branches that are rare at the reference's scenes marked for the compiler (block layout and the
- * register allocator's spill placement favour the other side); VPT_BRANCH_HINTS=0: no hints */
-#ifndef VPT_BRANCH_HINTS
-#define VPT_BRANCH_HINTS 1
-#endif
-#if VPT_BRANCH_HINTS
+ * register allocator's spill placement favour the other side) */
 #define VPT_UNLIKELY(c) __builtin_expect(!!(c), 0)
 #define VPT_LIKELY(c) __builtin_expect(!!(c), 1)
-#else
-#define VPT_UNLIKELY(c) (c)
-#define VPT_LIKELY(c) (c)
-#endif
 
-/* timing experiment only (NOT bit-exact): the intersection tests' square roots approximated */
-#ifndef VPT_ISECT_SQRT_APPROX
-#define VPT_ISECT_SQRT_APPROX 0
-#endif
-#if VPT_ISECT_SQRT_APPROX
-#define ISECT_SQRT(x) ((x) * __builtin_amdgcn_rsq(x))
-#else
 #define ISECT_SQRT(x) vm_sqrt(x)
-#endif
 
 /* Debug section timers (builds with -DVPT_SECTIONS=1 only; scripts/sect_stats.py): the wave's
  * s_memtime cycles spent in each section, accumulated per
@@ -197,20 +167,11 @@ VPT_DEV double sphere_tact(double b, double det)
     return tact;
 }
 
-/* the nearest-contact update of intersect() (include/pathTracingUtilities.h:17-30).  VPT_TAKE_BF=1:
- * written with selects (A/B: 56.8 -> 57.7 ms at FF 1024^2 x 256, slower) */
-#ifndef VPT_TAKE_BF
-#define VPT_TAKE_BF 0
-#endif
+/* the nearest-contact update of intersect() (include/pathTracingUtilities.h:17-30); branches, not
+ * selects (A/B round 2: 56.8 vs 57.7 ms with selects at FF 1024^2 x 256) */
 VPT_DEV void sphere_take(double tact, int i, double& tmin, int& id, int& contact)
 {
-    if (VPT_TAKE_BF) {
-        const bool hit = tact > 0.0001;
-        const bool upd = hit && tact < tmin;
-        contact |= (int)hit;
-        tmin = upd ? tact : tmin;
-        id = upd ? i : id;
-    } else if (tact > 0.0001) {
+    if (tact > 0.0001) {
         contact = 1;
         if (tact < tmin) {
             tmin = tact;
@@ -258,6 +219,7 @@ template <int G, bool COUNT>
 VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, double& t,
                                     int& id)
 {
+    static_assert(G >= 1, "spheres are taken G >= 1 at a time");
     double tmin = VPT_DBL_MAX;
     int contact = 0;
     const int n = S->n;
@@ -274,16 +236,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         }
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            double tact;
-            if (VPT_BF_G) {  /* branch-free: the G square-root chains overlap (same values where det >= 0) */
-                const double sq = ISECT_SQRT(det[k] >= 0 ? det[k] : 0.0);
-                const double t2 = -b[k] + sq;
-                const double t1 = -b[k] - sq;
-                tact = det[k] >= 0 ? (t1 < 0.0001 ? t2 : t1) : 0.0;
-            } else {
-                tact = sphere_tact(b[k], det[k]);
-            }
-            sphere_take(tact, i + k, tmin, id, contact);
+            sphere_take(sphere_tact(b[k], det[k]), i + k, tmin, id, contact);
         }
     }
     for (; i < n; ++i) {
@@ -310,6 +263,7 @@ template <int G, bool COUNT>
 VPT_DEV int scene_intersect_grouped_oc(const DevScene* __restrict__ S, Sampler<COUNT>& smp, const double (*oc)[4],
                                        dv3 d, double& t, int& id)
 {
+    static_assert(G >= 1, "spheres are taken G >= 1 at a time");
     double tmin = VPT_DBL_MAX;
     int contact = 0;
     const int n = S->n;
@@ -354,56 +308,16 @@ __device__ static inline void march_origin_init(const DevScene* __restrict__ S, 
     }
 }
 
-/* every intersection site (not only decide) through the grouped loop (A/B knob) */
+/* every intersection site (not only decide) through the grouped loop, G spheres at a time */
 #ifndef VPT_ISECT_GROUP_ALL
 #define VPT_ISECT_GROUP_ALL 5
 #endif
-/* intersect() out of line (VPT_ISECT_CALL): one copy of the sphere loop serves every site instead of
- * ~3 KB of unrolled loop per site -- the kernel's hot code, not its arithmetic, is what a smaller
- * copy count buys (the instruction cache is shared by two CUs).  The callee's registers are the
- * caller-saved ones, so the caller keeps its live values in place across the call. */
-#ifndef VPT_ISECT_CALL
-#define VPT_ISECT_CALL 0  /* A/B: FF 55.29 -> 56.11 ms, MIS 257.8 -> 277.2 (with VPT_ONE_A) */
-#endif
-struct IsectR {
-    double t;
-    int id, hit;
-};
-__device__ static __attribute__((noinline)) IsectR isect_ool(const DevScene* __restrict__ S, dv3 o, dv3 d, int id0)
-{
-    /* the scene pointer is wave-uniform: back to SGPRs, so that the sphere records come through
-     * scalar loads as in the inlined loop */
-    const uint64_t pv = (uint64_t)S;
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pv >> 32));
-    const DevScene* __restrict__ Su = (const DevScene*)(((uint64_t)hi << 32) | lo);
-    Sampler<false> smp;
-    IsectR r;
-    r.id = id0;
-#if VPT_ISECT_GROUP_ALL > 1
-    r.hit = scene_intersect_grouped<VPT_ISECT_GROUP_ALL>(Su, smp, o, d, r.t, r.id);
-#else
-    r.hit = scene_intersect(Su, smp, o, d, r.t, r.id, false);
-#endif
-    return r;
-}
-
+static_assert(VPT_ISECT_GROUP_ALL >= 1, "spheres are taken G >= 1 at a time");
 template <bool COUNT>
 VPT_DEV int scene_isect(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, double& t, int& id,
                         bool skip3)
 {
-#if VPT_ISECT_CALL && defined(__HIP_DEVICE_COMPILE__)
-    if (!skip3) {
-        const IsectR r = isect_ool(S, o, d, id);
-        smp.tests(S->n);
-        t = r.t;
-        id = r.id;
-        return r.hit;
-    }
-#endif
-#if VPT_ISECT_GROUP_ALL > 1
     if (!skip3) return scene_intersect_grouped<VPT_ISECT_GROUP_ALL>(S, smp, o, d, t, id);
-#endif
     return scene_intersect(S, smp, o, d, t, id, skip3);
 }
 
@@ -491,12 +405,6 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
 }
 
 /* ------------------------------------------------------------------ sampling */
-#ifndef VPT_POINT_H5
-#define VPT_POINT_H5 1    /* single_scattering: a point light's cone hit scores +-0 without computing it */
-#endif
-#ifndef VPT_POINT_CONE
-#define VPT_POINT_CONE 1  /* dir_from_cos: the cone toward a point light without its trig and frame (exact) */
-#endif
 /* direction at polar angle theta = acos(c) and azimuth phi around n: the reference computes
  * sin(acos c), cos(acos c), sin(phi), cos(phi) with libm (lm_dir_trig, bit for bit) */
 VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
@@ -511,7 +419,7 @@ VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
         /* ... and when no component of n is zero, not even those: from_local(n, 0 cp, 0 sp, 1) =
          * (s (+-0) + t (+-0)) + n 1 = n exactly (the frame of a unit n is finite, so s and t scale
          * to signed zeros, which a nonzero n_k absorbs) -- the azimuth draw is taken by the caller */
-        if (VPT_POINT_CONE && __ballot(n.x == 0 || n.y == 0 || n.z == 0 || !(n.x - n.x == 0 && n.y - n.y == 0 && n.z - n.z == 0)) == 0)
+        if (__ballot(n.x == 0 || n.y == 0 || n.z == 0 || !(n.x - n.x == 0 && n.y - n.y == 0 && n.z - n.z == 0)) == 0)
             return nrm(n);
         lm_sincos(phi, &sp, &cp);
     } else {
@@ -648,18 +556,10 @@ VPT_DEV double microfacet_prob(dv3 wo, dv3 wh, double alpha, dv3 n)
     return ndf(dot(wh, n), alpha) * num / den;
 }
 
-/* frMicroFacet, :95-100 (G_smith :63-68).  Out of line on the device (VPT_FR_CALL): three Fresnel
- * channels, two Smith terms and the NDF are independent chains that the scheduler interleaves, and
- * inlined at the five sites of a metal surface event they set the kernel's register allocation. */
-#ifndef VPT_FR_CALL
-#define VPT_FR_CALL 1       /* with VPT_FUSE_RARE_MONO (A/B above); round-2 tree: 53.28 vs 53.50 ms FF */
-#endif
-#if VPT_FR_CALL
-#define VPT_FR_QUAL __device__ static __attribute__((noinline))
-#else
-#define VPT_FR_QUAL VPT_DEV
-#endif
-VPT_FR_QUAL dv3 fr_microfacet(dv3 eta, dv3 kappa, dv3 wi, dv3 wh, dv3 wo, double alpha, dv3 n)
+/* frMicroFacet, :95-100 (G_smith :63-68).  Out of line: three Fresnel channels, two Smith terms and
+ * the NDF are independent chains that the scheduler interleaves, and inlined at the five sites of a
+ * metal surface event they set the kernel's register allocation (A/B round 3: 53.28 vs 53.50 ms FF) */
+__device__ static __attribute__((noinline)) dv3 fr_microfacet(dv3 eta, dv3 kappa, dv3 wi, dv3 wh, dv3 wo, double alpha, dv3 n)
 {
     double den = (4 * vm_fabs(dot(n, wi)) * vm_fabs(dot(n, wo)));
     double G = g1(n, wi, wh, alpha) * g1(n, wo, wh, alpha);
@@ -694,22 +594,11 @@ VPT_DEV dv3 refrax_dielectric(double etai, double etat, dv3 wi, dv3 n)
  * a per-lane load of the GeoSphere record (whose latency sat on decide()'s critical path) */
 VPT_DEV int sph_flag(uint64_t m, int i) { return (int)((m >> (i & 63)) & 1ull); }
 
-/* the emitter list's entry j (vptShadeMethods.h:1293-1303, idsource = arr[rand * count]): up to 8
- * emitters by selects over scalar loads, else a per-lane load */
-#ifndef VPT_EMIT_SELECT
-#define VPT_EMIT_SELECT 0  /* 1: selects over scalar loads for <= 8 emitters (A/B 50.58 -> 51.20 ms FF, 222.9 -> 226.9 MIS: slower) */
-#endif
-VPT_DEV int emit_pick(const DevScene* __restrict__ S, int j, int count)
+/* the emitter list's entry j (vptShadeMethods.h:1293-1303, idsource = arr[rand * count]): a per-lane
+ * load (selects over scalar loads were slower: A/B round 3, 50.58 -> 51.20 ms FF) */
+VPT_DEV int emit_pick(const DevScene* __restrict__ S, int /*count*/ j, int count)
 {
-#if VPT_EMIT_SELECT
-    if (count <= 8) {
-        int src = S->emit[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k)
-            if (k < count) src = j == k ? S->emit[k] : src;
-        return src;
-    }
-#endif
+    (void)count;
     return S->emit[j];
 }
 
@@ -906,16 +795,7 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
         for (int k = 0; k < N; ++k) {
             const double b = ocx * d[k].x + ocy * d[k].y + ocz * d[k].z;
             const double det = b * b - cc + g.r2;
-            double tact;
-            if (VPT_BF_N) {  /* branch-free: the N rays' square-root chains overlap */
-                const double sq = ISECT_SQRT(det >= 0 ? det : 0.0);
-                const double t2 = -b + sq;
-                const double t1 = -b - sq;
-                tact = det >= 0 ? (t1 < 0.0001 ? t2 : t1) : 0.0;
-            } else {
-                tact = sphere_tact(b, det);
-            }
-            sphere_take(tact, i, tmin[k], id[k], contact[k]);
+            sphere_take(sphere_tact(b, det), i, tmin[k], id[k], contact[k]);
         }
     }
     smp.tests(N * n);
@@ -990,22 +870,9 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     double tt[3];
     int ids[3] = {0, 0, 0};
     bool hits[3];
-#if VPT_FUSE_RAYS == 3
     SECT_BEGIN(mi);
     scene_intersect_n<3>(S, smp, x, dirs, tt, ids, hits);
     SECT_END(mi, SECT_S_MIS_ISECT);
-#else
-    {
-        const dv3 d2[2] = {dirs[0], dirs[1]};
-        double t2[2];
-        int i2[2] = {0, 0};
-        bool h2[2];
-        scene_intersect_n<2>(S, smp, x, d2, t2, i2, h2);
-        ids[0] = i2[0];
-        ids[1] = i2[1];
-        hits[2] = scene_intersect(S, smp, x, dirs[2], tt[2], ids[2], false);
-    }
-#endif
     /* ---- the reference's arithmetic */
     dv3 mc = mk(0, 0, 0);
     double fpdf = 0, gpdf = 0, cmax = 0, wg;
@@ -1189,7 +1056,7 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         /* a point light's cone (cmax == 1: prob_wl = +inf) scores Ls * (1 / inf) = +-0 with Ls finite
          * (SURVEY H5); zero_ok: the caller's update absorbs a signed zero (finite throughput and
          * pdf), so +0 is the same result without the exponential and the phase value */
-        if (!(LT == 1 && VPT_POINT_H5 && zero_ok && cmax == 1.0)) {
+        if (!(LT == 1 && zero_ok && cmax == 1.0)) {
             double it = lm_exp(sigma_t * tdist * -1.0);
             double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, wl);
             dv3 Ls = scl(scl(rad, it), ph);
@@ -1240,12 +1107,6 @@ VPT_DEV double equiangular_params2(const DevScene* __restrict__ S, Sampler<COUNT
  * equi-angular arithmetic (two atan2, a tan, the pdf) runs in the medium event only -- a surface
  * event (a third of them) never reads it.  The draw rides in Event::pdf, its sign bit marking a
  * ray that hit nothing (EST 4's psurf is 0 there). */
-#ifndef VPT_PLIGHT_SKIP
-#define VPT_PLIGHT_SKIP 1   /* surface_event: pLight toward a sphere light skipped when exactly zero in every lane */
-#endif
-#ifndef VPT_EQA_DEFER
-#define VPT_EQA_DEFER 1
-#endif
 
 /* equiAngularProb, include/vptSamplingFunctions.h:60-62 */
 VPT_DEV double equiangular_prob(double D, double ta, double tb, double s) { return D / vm_fabs(tb - ta) / (s * s + D * D); }
@@ -1312,13 +1173,7 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
     int id = 0;
     double t;
     SECT_BEGIN(di);
-#if VPT_ISECT_CALL && defined(__HIP_DEVICE_COMPILE__)
-    const bool hit = scene_isect(S, smp, p.o, p.d, t, id, false);
-#elif VPT_DECIDE_GROUP > 1
     const bool hit = scene_intersect_grouped<VPT_DECIDE_GROUP>(S, smp, p.o, p.d, t, id);
-#else
-    const bool hit = scene_intersect(S, smp, p.o, p.d, t, id, false);
-#endif
     SECT_END(di, SECT_A_ISECT);
     if constexpr (EST == 5) {  /* iterativePathTracer (shadeMethods.h:115-125): nearest hit or end */
         if (COUNT) smp.cnt.iterations++;
@@ -1358,13 +1213,9 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
         /* MIS: psurf = exp(-σt t) (:1419); explicit: TrActual = Tr(x, xs), 0 on a miss (:1033-1041) */
         const double psurf = EST == 1 ? lm_exp(sigma_t * t * -1.0)
                                       : (hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0);
-        if (VPT_EQA_DEFER) {
+        {
             const double x = smp.next();  /* equiAngularParams2's draw (volumetricBasicFunctions.h:219) */
             e.pdf = hit ? x : -x;          /* medium_event: eqa_medium */
-        } else {
-            double D = 0, ta = 0, tb = 0, sd = 0;
-            e.dist = equiangular_params2(S, smp, e.src, t, p.o, p.d, D, ta, tb, sd);
-            e.pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
         }
         surf = EST == 1 ? smp.next() < psurf : smp.next() <= psurf;  /* :1423 / :1096 */
     }
@@ -1409,7 +1260,7 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
      * Ldp + Ld == Ld: when that holds in every lane of the wave, the frames, the normalisations and
      * the transmittance of pLight are skipped -- same bits, no draws involved. */
     bool plight_zero = false;
-    if (VPT_PLIGHT_SKIP && PT == 0 && S->n_mat3 == 0) {
+    if (PT == 0 && S->n_mat3 == 0) {
         const dv3 lx = sub(sph_p(S, src), xs);
         const double dd = dot(lx, lx);
         const double distance = vm_sqrt(dd);  /* visibility()'s test, pathTracingUtilities.h:44-51 */
@@ -1424,13 +1275,10 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     }
     SECT_END(pl, SECT_S_PLIGHT);
     SECT_BEGIN(mis);
-#if VPT_FUSE_RAYS
-    dv3 Ld = (MK == 0 || !VPT_FUSE_RARE_MONO) && S->n_mis == 2
-                 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
-                 : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
-#else
-    dv3 Ld = mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
-#endif
+    /* the fused three-ray MISv2 for diffuse surfaces only: metal and dielectric take the sequential
+     * one (round 3: scratch 448 -> 240 B/lane, FF 51.99 -> 51.53 ms) */
+    dv3 Ld = MK == 0 && S->n_mis == 2 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
+                                      : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
     SECT_END(mis, SECT_S_MIS);
     SECT_BEGIN(bd);
     dv3 wi = mk(0, 0, 0);
@@ -1483,7 +1331,7 @@ VPT_DEV bool surface_event_pt(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     return false;
 }
 
-/* the deferred equi-angular arithmetic of decide() (VPT_EQA_DEFER): d_final and its pdf from the
+/* the deferred equi-angular arithmetic of decide(): d_final and its pdf from the
  * ray, the light, tMax = e.t and the draw carried in e.pdf -- the operations decide() performed in
  * round 2, in the same order */
 template <int EST>
@@ -1508,7 +1356,7 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
     const double continueprob = 0.6;
     Event e = e0;
     SECT_BEGIN(eq);
-    if (VPT_EQA_DEFER && (EST == 1 || EST == 4)) eqa_medium<EST>(S, p, e0, sigma_t, e.dist, e.pdf);
+    if (EST == 1 || EST == 4) eqa_medium<EST>(S, p, e0, sigma_t, e.dist, e.pdf);
     SECT_END(eq, SECT_M_EQA);
     dv3 xt = add(p.o, scl(p.d, e.dist));
     if (EST == 3) {  /* implicit: vptShadeMethods.h:1000-1006 */

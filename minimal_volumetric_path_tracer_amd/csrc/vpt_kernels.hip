@@ -50,9 +50,6 @@ struct KParams {
             return vpt_fail(VPT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));       \
     } while (0)
 
-#ifndef VPT_MARCH_OC
-#define VPT_MARCH_OC 1
-#endif
 template <int EST, bool COUNT, int FB>
 __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const DevScene* __restrict__ S)
 {
@@ -60,9 +57,9 @@ __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const Dev
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     /* rayMarching3: every shadow ray leaves the light's centre, so oc and |oc|^2 of each sphere are
-     * formed once per workgroup (VPT_MARCH_OC) */
-    __shared__ double march_oc[EST == 6 && VPT_MARCH_OC ? VPT_MAX_SPHERES : 1][4];
-    if (EST == 6 && VPT_MARCH_OC) {
+     * formed once per workgroup (round 3: 26.7 -> 32.4 Msamples/s) */
+    __shared__ double march_oc[EST == 6 ? VPT_MAX_SPHERES : 1][4];
+    if (EST == 6) {
         march_origin_init(S, sph_p(S, P.march_light), march_oc);
         __syncthreads();
     }
@@ -87,7 +84,7 @@ __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const Dev
         double jy = smp.next();
         dv3 dir = add(add(scl(cx, (((double)x + jx - 0.5) / P.w - .5)), scl(cy, (((double)y + jy - 0.5) / P.h - .5))), cd);
         dir = nrm(dir);
-        dv3 L = trace_sample<EST, COUNT>(S, smp, o, dir, m, EST == 6 && VPT_MARCH_OC ? march_oc : nullptr);
+        dv3 L = trace_sample<EST, COUNT>(S, smp, o, dir, m, EST == 6 ? march_oc : nullptr);
         acc = add(L, acc);
         if (COUNT) {
             tests += smp.cnt.tests;
@@ -395,6 +392,7 @@ struct StreamSlot {
 /* at most this many slots (each holds a partials buffer): a further stream takes over the least
  * recently used slot whose work has finished, or waits for the least recently used one */
 constexpr int MAX_STREAM_SLOTS = 8;
+constexpr int LAUNCH_LOG2_MAX = 26;  /* samples per workgroup per pool launch <= 2^26 (launch_max_units) */
 
 struct vpt_context {
     int device;
@@ -405,6 +403,7 @@ struct vpt_context {
     std::mutex mu;           /* guards slots: held from taking a slot until its launches are enqueued */
     std::vector<std::unique_ptr<StreamSlot>> slots;  /* stable addresses */
     unsigned long long tick = 0;
+    int launch_log2 = LAUNCH_LOG2_MAX;  /* samples per workgroup per launch <= 2^launch_log2 (vpt_debug_set_launch_bound) */
 };
 
 /* The stream's slot, created on first use (or taken over from an idle stream once MAX_STREAM_SLOTS
@@ -577,13 +576,21 @@ static int launch_wave(vpt_context* ctx, KParams K, hipStream_t stream);
 template <int EST, int FB>
 static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream);
 
-/* log2(v) when v is a power of two, else -1 (PoolParams shift fast paths; VPT_POW2=0: always -1, A/B) */
-#ifndef VPT_POW2
-#define VPT_POW2 1
-#endif
+/* The pool's ring positions are 32-bit counters that grow by ~3 per sample a workgroup runs, so a
+ * render is split into launches of at most 2^LAUNCH_LOG2_MAX samples per workgroup: units in order
+ * [unit0, unit0 + nunits), each unit one partial slot, so the split changes no value (the chunk
+ * sums are per unit; reduce_kernel adds them after the last launch).  One launch holds up to
+ * ~17 G samples on 256 CUs; BASELINE configs[4] (2^34 samples per GPU) takes two. */
+static uint64_t launch_max_units(int blocks, int C, int log2_bound)
+{
+    const uint64_t m = (((uint64_t)1 << log2_bound) * (uint64_t)(blocks > 0 ? blocks : 1)) / (uint64_t)(C > 0 ? C : 1);
+    return m < 1 ? 1 : m;
+}
+
+/* log2(v) when v is a power of two, else -1 (PoolParams shift fast paths) */
 static int log2_exact(int64_t v)
 {
-    if (!VPT_POW2 || v <= 0 || (v & (v - 1)) != 0) return -1;
+    if (v <= 0 || (v & (v - 1)) != 0) return -1;
     int k = 0;
     while ((v >> k) != 1) ++k;
     return k;
@@ -663,14 +670,11 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         /* every workgroup adds UREFILL to the u32 queue once more after it runs dry */
         if (units + (uint64_t)blocks * (UREFILL + 1) >= 0xFFFFFFFFull)
             return vpt_fail(VPT_E_INVALID, "too many work units (%llu) for the u32 work queue", (unsigned long long)units);
-        /* The pool's ring positions are 32-bit counters that grow by ~3 per sample a workgroup
-         * runs: launches are capped at 2^26 samples per workgroup (units in order, one partial
-         * slot each, so splitting changes no value); one launch up to ~17 G samples on 256 CUs. */
-        /* (samples per unit: at most the layout's head chunk C; a unit above 2^26 samples is refused) */
-        if (Q.lay.C > (1 << 26))
+        /* launches of at most 2^launch_log2 samples per workgroup (launch_max_units); samples per
+         * unit: at most the layout's head chunk C, and a unit above 2^LAUNCH_LOG2_MAX is refused */
+        if (Q.lay.C > (1 << LAUNCH_LOG2_MAX))
             return vpt_fail(VPT_E_INVALID, "chunk of %d samples > 2^26 (the per-workgroup launch bound)", Q.lay.C);
-        uint64_t max_units = (((uint64_t)1 << 26) * (uint64_t)blocks) / (uint64_t)(Q.lay.C > 0 ? Q.lay.C : 1);
-        if (max_units < 1) max_units = 1;
+        const uint64_t max_units = launch_max_units(blocks, Q.lay.C, ctx->launch_log2);
         unsigned long long* stats = nullptr;
         if (env_int("VPT_POOL_STATS", 0)) {  /* debug: scheduler statistics, vpt_debug_pool_stats */
             if (!g_pool_stats) HIP_OK(hipMalloc((void**)&g_pool_stats, (TL0 + 3 * TL_MAXWG) * sizeof(unsigned long long)));
@@ -1117,4 +1121,39 @@ extern "C" int vpt_debug_pool_timeline(unsigned long long* out)
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(out, g_pool_stats + TL0, 3 * TL_MAXWG * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return VPT_OK;
+}
+
+/* debug: the per-launch bound of ctx's pool renders lowered to 2^log2 samples per workgroup (0..26; 26 =
+ * the production bound), so that a small render takes the multi-launch path that BASELINE configs[4]
+ * (2^34 samples per GPU) takes in production (tests/test_gpu_parity.py).  Returns VPT_E_INVALID
+ * outside 0..26. */
+extern "C" int vpt_debug_set_launch_bound(vpt_context* ctx, int log2)
+{
+    if (!ctx || log2 < 0 || log2 > LAUNCH_LOG2_MAX) return vpt_fail(VPT_E_INVALID, "launch bound 2^%d outside 2^0..2^26", log2);
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->launch_log2 = log2;
+    return VPT_OK;
+}
+
+/* debug, host only (no GPU): the launches a pool render of p's shard makes on `blocks` workgroups with the
+ * bound 2^log2 -- the same units (tiles of 8 x 8 pixels x chunks, vpt_chunks.h) and the same split as
+ * launch_pool.  Writes up to cap (unit0, nunits) pairs; returns the number of launches, or < 0. */
+extern "C" int64_t vpt_debug_launch_plan(const vpt_params* p, int blocks, int log2, uint64_t* unit0, uint64_t* nunits,
+                                         int64_t cap)
+{
+    if (!p || blocks < 1 || log2 < 0 || log2 > LAUNCH_LOG2_MAX || p->spp <= 0 || p->width <= 0 || p->chunk_spp < 0)
+        return VPT_E_INVALID;
+    const int rows = vpt_shard_rows(p);
+    const int chunk = p->chunk_spp > 0 ? (p->chunk_spp < p->spp ? p->chunk_spp : p->spp) : vpt_auto_chunk(p->spp);
+    const vpt_chunk_layout lay = vpt_chunks(p->spp, chunk, p->chunk_spp == 0);
+    const uint64_t units = (uint64_t)((p->width + 7) / 8) * (uint64_t)((rows + 7) / 8) * 64u * (uint64_t)lay.n;
+    const uint64_t max_units = launch_max_units(blocks, lay.C, log2);
+    int64_t k = 0;
+    for (uint64_t u0 = 0; u0 < units; u0 += max_units, ++k) {
+        if (k < cap && unit0 && nunits) {
+            unit0[k] = u0;
+            nunits[k] = units - u0 < max_units ? units - u0 : max_units;
+        }
+    }
+    return k;
 }

@@ -81,9 +81,6 @@ void sync_all(vpt_multi* m)
 
 }  // namespace
 
-extern "C" {
-
-}  // extern "C"
 
 namespace {
 

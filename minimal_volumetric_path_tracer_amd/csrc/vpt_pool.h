@@ -13,10 +13,11 @@
  *     ring 0     stage A
  *     ring 1..4  stage S: diffuse surface + sphere light, diffuse + point light, metal, other
  *     ring 5..6  stage M: sphere light, point light
- * A wave takes the workgroup's ticket lock, returns its finished tasks to the rings of their next
- * stage, takes up to 64 tasks of the fullest ring, releases the lock, loads those states, runs
- * that ONE stage with (nearly) every lane busy, and stores the states back.  The pool is larger
- * than the workgroup (880 tasks for 512 lanes), so there is nearly always a full batch of some ring.
+ A wave returns its finished tasks to the rings of their next stage (lock-free: one LDS atomic per
+ * ring reserves positions), claims up to 64 tasks of the fullest ring (one CAS on its head), runs
+ * that ONE stage with (nearly) every lane busy -- an S/M batch then runs stage A on the same lanes --
+ * and stores the states back.  The pool is larger than the workgroup (880 tasks for 512 lanes), so
+ * there is nearly always a full batch of some ring.
  *
  * Determinism: a task runs its unit's samples strictly in order and adds each sample to the
  * chunk sum as the reference adds to its pixel (acc = L + acc, src/rt.cpp:794); chunk sums are
@@ -50,33 +51,6 @@ namespace vpt {
 #ifndef VPT_SCHED_PRIO
 #define VPT_SCHED_PRIO 3    /* s_setprio level of the scheduler's critical section (0: off; A/B 3 vs 0: +0.7 %) */
 #endif
-#ifndef VPT_FUSE_A
-#define VPT_FUSE_A 1        /* stage A run by the S/M wave on its own batch (0: via ring A) */
-#endif
-#ifndef VPT_LOCKFREE
-#define VPT_LOCKFREE 1      /* rings without the ticket lock (ring_entry) */
-#endif
-#ifndef VPT_LATE_UNIT
-#define VPT_LATE_UNIT 0     /* 1: stage-A-only task fields loaded after the S/M body (A/B: 5674 vs 5757 Ms/s, slower) */
-#endif
-#ifndef VPT_SHFL_LEADER
-#define VPT_SHFL_LEADER 0   /* 1: stage A's unit-ring leader values broadcast by __shfl (LDS permute), 0: v_readlane */
-#endif
-#ifndef VPT_RUN_EVENT_ORDER
-#define VPT_RUN_EVENT_ORDER 0  /* 1: the rare surface rings tested first (with VPT_RARE_HINT); 0: index order (A/B 55.71 ms / 269.8) */
-#endif
-#ifndef VPT_SCHED_FAST
-#define VPT_SCHED_FAST 0    /* 1: scheduler with one counter read per batch and ring bases by v_readlane (A/B 51.48 -> 51.65 ms FF: no gain) */
-#endif
-#ifndef VPT_MERGE_LIGHTS
-#define VPT_MERGE_LIGHTS 0  /* bit 0: the diffuse surface rings' code shared by both light kinds; bit 1: the medium rings' */
-#endif
-#ifndef VPT_ONE_A
-#define VPT_ONE_A 1         /* 1: one inlined copy of stage A (ring-A and fused S/M batches share it; A/B FF 53.45 -> 55.29 ms, MIS 260.7 -> 257.8) */
-#endif
-#if VPT_ONE_A && (!VPT_FUSE_A || VPT_LATE_UNIT)
-#error "VPT_ONE_A needs VPT_FUSE_A=1 and VPT_LATE_UNIT=0"
-#endif
 #ifndef VPT_PREP_TRIES
 #define VPT_PREP_TRIES 2    /* samples a lane may start per preparation round (A/B 1 / 2 / 4 / 8: FF 52.16 / 52.02 / 53.70 / 53.85 ms, MIS 248.1 / 245.2 / 251.9 / 252.0) */
 #endif
@@ -90,9 +64,6 @@ namespace vpt {
  * 0 (always a second round) 49.87 / 222.4; 8 48.46 / 216.1; 16 48.41 / 216.1; 24 48.39 / 215.9;
  * 32 48.39 / 215.9; one round only (VPT_PREP_ROUNDS=1) 48.11 / 218.1 */
 #define VPT_PREP_MORE_MIN 24
-#endif
-#ifndef VPT_RING_MASK
-#define VPT_RING_MASK 0x7E  /* register-pressure probes only (wrong images otherwise): bit r compiles the S/M code of ring r */
 #endif
 constexpr int POOL = VPT_POOL_SIZE; /* task slots per workgroup: 182 B each + ~1.1 KB (161 KB at 880) */
 constexpr int NF = 18;      /* doubles per task */
@@ -112,7 +83,7 @@ static_assert(URING >= 2 * UREFILL, "a refill (at most UREFILL entries from utai
 /* debug statistics, in builds with -DVPT_POOL_DEBUG=1 (=2: top-level cycle split only, cheaper;
  * scripts/build_variant.sh) run with
  * VPT_POOL_STATS=1 (vpt_debug_pool_stats, scripts/pool_stats.py): [0-6] batches per ring, [7-13] lanes
- * per ring, [14] idle polls, [15] ticket waits, [16-19] cycles in stage A/S/M/scheduling, [20]
+ * per ring, [14] idle polls, [15] claim retries, [16-19] cycles in stage A/S/M/scheduling, [20]
  * stage-A preparation rounds, [21] samples started, [22] cycles preparing, [23] cycles in decide */
 constexpr int NSTATS = 24;
 /* debug timeline (s_memrealtime, 100 MHz) after the counters: per workgroup b, stats[TL0 + 3b + k] =
@@ -144,11 +115,10 @@ struct TaskPool {
     /* the scheduler's counters, contiguous so that one lane-parallel LDS read fetches them all:
      * monotonic ring tails and heads, slots retired, the unit ring's tail, queue exhausted */
     int ctl[NCTL];
-    int ticket, serving;     /* FIFO ticket lock: a wave returning tasks is never starved */
-    uint32_t uring[URING];   /* prefetched work units (refilled under the lock, taken by CAS on ctl[C_UHEAD]) */
+    uint32_t uring[URING];   /* prefetched work units (refilled by one wave at a time under the C_RFL flag, taken by CAS on ctl[C_UHEAD]) */
 };
 
-/* Lock-free rings (VPT_LOCKFREE): an entry is the slot and the lap of its ring position,
+/* Lock-free rings: an entry is the slot and the lap of its ring position,
  * slot | (position / POOL mod 128) << 9.  A producer reserves positions with one atomic add on the
  * ring's tail and then writes the entries; a consumer reads entries from the head, keeps the prefix
  * whose lap tags are current (written), and claims exactly that prefix with one CAS on the head.
@@ -308,45 +278,9 @@ __device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t
     P.partials[o + 2] = t.acc.z;
 }
 
-/* Out-of-line surface events for the rare surface rings (metal, other materials).  Inlined, their
- * shading (microfacet BSDF in pLight, MISv2 and bdsf; 210 / 145 VGPRs spilled on their own) set the
- * register allocation of the whole kernel -- 315 VGPRs spilled, whose reloads sit in the hot rings
- * too.  As a call, their pressure stays inside the callee; the path state crosses through private
- * temporaries (copied in and out, so the caller's task keeps living in registers). */
-#ifndef VPT_RARE_CALL
-#define VPT_RARE_CALL 0     /* A/B: FF 53.50 -> 61.91 ms, MIS 260.9 -> 303.3 ms (calls force every live value around them) */
-#endif
-#ifndef VPT_RARE_HINT
-#define VPT_RARE_HINT 0     /* the rare surface rings marked unlikely (A/B with VPT_RUN_EVENT_ORDER=1: FF 56.68 -> 53.95 ms, MIS 275.7 -> 259.4) */
-#endif
-template <int EST, bool COUNT, int MK>
-__device__ __attribute__((noinline)) void surface_event_ool(const DevScene* __restrict__ S, Sampler<COUNT>* smp, Path* p,
-                                                            const Event* e, const Medium* m)
-{
-    surface_event<EST, COUNT, MK, -1>(S, *smp, *p, *e, *m);
-}
-
-template <int EST, bool COUNT, int MK>
-__device__ __forceinline__ void surface_event_rare(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
-                                                   const Event& e, const Medium& m)
-{
-#if VPT_RARE_CALL
-    Sampler<COUNT> sm = smp;
-    Path pp = p;
-    Event ee = e;
-    Medium mm = m;
-    surface_event_ool<EST, COUNT, MK>(S, &sm, &pp, &ee, &mm);
-    smp = sm;
-    p = pp;
-#else
-    surface_event<EST, COUNT, MK, -1>(S, smp, p, e, m);
-#endif
-}
-
 /* The S or M event of ring st (1-6) for one task, then the next iteration's roulette draw.  Surface
  * rings are keyed by material -- diffuse (R_S, R_S + 1), metal (R_S + 2), other -- and by light kind:
  * sphere light (R_S, R_M), point light (R_S + 1, R_M + 1). */
-#define VPT_RING_ON(r) ((VPT_RING_MASK >> (r)) & 1)
 template <int EST, bool COUNT>
 __device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Task& t, const Medium& m, int st)
 {
@@ -356,26 +290,17 @@ __device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sample
         else t.killed = surface_event_pt<COUNT, -1>(S, smp, t.p, t.e);
     } else {
         SECT_BEGIN(ev);
+        /* metal (R_S + 2) and other materials (R_S + 3) are rare: 1.4 % of surface events at the
+         * bench scene */
         if (st < R_M) {
-            /* metal and other materials: rare (1.4 % of surface events at the bench scene) */
-            if (!VPT_RUN_EVENT_ORDER) {  /* round-2 order: the rings in index order */
-                if (st == R_S) { if (VPT_RING_ON(1)) surface_event<EST, COUNT, 0, (VPT_MERGE_LIGHTS & 1) ? -1 : 0>(S, smp, t.p, t.e, m); }
-                else if (st == R_S + 1) { if (VPT_RING_ON(2)) surface_event<EST, COUNT, 0, (VPT_MERGE_LIGHTS & 1) ? -1 : 1>(S, smp, t.p, t.e, m); }
-                else if (st == R_S + 2) { if (VPT_RING_ON(3)) surface_event_rare<EST, COUNT, 1>(S, smp, t.p, t.e, m); }
-                else { if (VPT_RING_ON(4)) surface_event_rare<EST, COUNT, -1>(S, smp, t.p, t.e, m); }
-            } else if (VPT_RARE_HINT ? __builtin_expect(st >= R_S + 2, 0) : st >= R_S + 2) {
-                if (st == R_S + 2) { if (VPT_RING_ON(3)) surface_event_rare<EST, COUNT, 1>(S, smp, t.p, t.e, m); }
-                else { if (VPT_RING_ON(4)) surface_event_rare<EST, COUNT, -1>(S, smp, t.p, t.e, m); }
-            } else if ((VPT_MERGE_LIGHTS & 1) || st == R_S) {
-                /* merged: one copy for both light kinds (the light's radius decides, uniformly per batch) */
-                if (VPT_RING_ON(1)) surface_event<EST, COUNT, 0, (VPT_MERGE_LIGHTS & 1) ? -1 : 0>(S, smp, t.p, t.e, m);
-            } else {
-                if (VPT_RING_ON(2)) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
-            }
-        } else if ((VPT_MERGE_LIGHTS & 2) || st == R_M) {
-            if (VPT_RING_ON(5)) medium_event<EST, COUNT, (VPT_MERGE_LIGHTS & 2) ? -1 : 0>(S, smp, t.p, t.e, m);
+            if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m);
+            else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
+            else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
+            else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
+        } else if (st == R_M) {
+            medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
         } else {
-            if (VPT_RING_ON(6)) medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
+            medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
         }
         SECT_END(ev, st < R_M ? SECT_S_TOTAL : SECT_M_TOTAL);
         SECT_BEGIN(cp);
@@ -434,15 +359,9 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                     got = max(0, min(k, avail));
                 }
                 /* leader is wave-uniform: v_readlane, not an LDS permute round trip */
-#if VPT_SHFL_LEADER
-                h = __shfl(h, leader);
-                got = __shfl(got, leader);
-                ex = __shfl(ex, leader);
-#else
                 h = __builtin_amdgcn_readlane(h, leader);
                 got = __builtin_amdgcn_readlane(got, leader);
                 ex = __builtin_amdgcn_readlane(ex, leader);
-#endif
                 if (need && r < got) ent = ((volatile uint32_t*)sh.uring)[(h + r) % URING];
                 if (got == 0) break;
                 /* the entry reads above must complete before the claim below: a refill may rewrite
@@ -566,7 +485,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
             result = R_M + (EST == 3 ? 0 : sph_flag(S->m_point, t.e.src));
             /* one slot (F_TD): stage M reads the sampled distance -- or, for the deferred
              * equi-angular estimators, tMax (with the draw in F_PDF) */
-            if (!(VPT_EQA_DEFER && (EST == 1 || EST == 4))) t.e.t = t.e.dist;
+            if (!(EST == 1 || EST == 4)) t.e.t = t.e.dist;
         }
         SECT_END(dci, SECT_A_DECIDE_IN);
     }
@@ -593,9 +512,6 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         for (int r = 1; r < NR; ++r) sh.ring[r][j] = (uint16_t)(LAP_MASK << SLOT_BITS);  /* no lap-0 entry yet */
     }
     if (tid < NCTL) sh.ctl[tid] = tid == C_TAIL + R_A ? POOL : 0;  /* every slot starts in ring A */
-    if (tid == 0) {
-        sh.ticket = sh.serving = 0;
-    }
     sect_init();
     __syncthreads();
 
@@ -614,7 +530,6 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
     if (dbg && tid == 0) dbg_tl(stats, 0, false);
     while (true) {
         SECT_BEGIN(sc);
-#if VPT_LOCKFREE
         /* ---- scheduling without a lock (ring_entry): reserve, publish, claim ---- */
         if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(VPT_SCHED_PRIO);
         if (n > 0) {  /* return the finished tasks: one LDS atomic per ring reserves their positions */
@@ -629,18 +544,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             int base = 0;
             if (lane < NR && cnt > 0)
                 base = __hip_atomic_fetch_add(&sh.ctl[C_TAIL + lane], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if VPT_SCHED_FAST
-            /* each lane's ring base from the lane that reserved it: v_readlane, not an LDS permute */
-            int bsel = 0;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const int br = __builtin_amdgcn_readlane(base, r);
-                bsel = next == r ? br : bsel;
-            }
-            const int pos = bsel + rank;
-#else
             const int pos = __shfl(base, ret ? next : 0) + rank;
-#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  /* task states before their entries */
             if (ret) ((volatile uint16_t*)sh.ring[next])[pos % POOL] = ring_entry(slot, pos);
             const uint64_t md = __ballot(lane < n && next == R_DONE);
@@ -649,17 +553,14 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         }
         /* keep the unit ring stocked (the queue atomic's latency is paid once per 128 units); one
          * wave at a time, claimed by a flag */
-        int v0 = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;  /* reused by the claim below (VPT_SCHED_FAST) */
-        bool reread = !VPT_SCHED_FAST;
         {
-            const int v = v0;
+            const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
             if (dbg && !seen_exh && __builtin_amdgcn_readlane(v, C_EXH)) {
                 seen_exh = true;
                 if (lane == 0) dbg_tl(stats, 1, false);
             }
             if (VPT_UNLIKELY(!__builtin_amdgcn_readlane(v, C_EXH) && !__builtin_amdgcn_readlane(v, C_RFL) &&
                 __builtin_amdgcn_readlane(v, C_UTAIL) - __builtin_amdgcn_readlane(v, C_UHEAD) < UREFILL)) {
-                reread = true;
                 int own = 0;
                 if (lane == 0) {
                     int z = 0;
@@ -691,8 +592,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         int st = 0, take = 0;
         bool fin = false;
         while (true) {
-            const int v = reread ? (lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0) : v0;
-            reread = true;
+            const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
             int best = 0;
             st = 0;
 #pragma unroll
@@ -747,105 +647,6 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         SECT_END(sc, SECT_SCHED);
         if (fin) break;
         n = take;
-#else
-        /* ---- an idle wave waits outside the lock until some ring has work (racy peek) ---- */
-        if (n == 0) {
-            bool fin = false;
-            while (true) {
-                const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
-                int pend = 0;
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    pend += __builtin_amdgcn_readlane(v, C_TAIL + r) - __builtin_amdgcn_readlane(v, C_HEAD + r);
-                if (pend > 0) break;
-                if (__builtin_amdgcn_readlane(v, C_DONE) == POOL) {
-                    fin = true;
-                    break;
-                }
-                ++st_idle;
-                __builtin_amdgcn_s_sleep(4);
-            }
-            if (fin) break;
-        }
-        /* ---- critical section: return finished tasks, take a batch of the fullest ring ---- */
-        int ticket = 0;
-        /* the critical section runs at raised issue priority: VALU issue between the two waves of
-         * a SIMD goes by priority, then age, and a lock holder starved by a computing partner wave
-         * holds up every other wave of its workgroup */
-        if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(VPT_SCHED_PRIO);
-        if (lane == 0) {
-            ticket = __hip_atomic_fetch_add(&sh.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            while (lds_peek(&sh.serving) != ticket) {
-                ++st_retry;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        /* all counters in one LDS read (lane k holds ctl[k]); positions, counts and the choice of
-         * ring are then worked out in registers, and the updates go back in two LDS writes */
-        int cv = lane < NCTL ? sh.ctl[lane] : 0;
-        if (n > 0) {
-            const bool ret = lane < n && next < NR;
-            int pos = 0;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const uint64_t msk = __ballot(ret && next == r);
-                if (msk) {
-                    const int tr = __builtin_amdgcn_readlane(cv, C_TAIL + r);
-                    if (ret && next == r) pos = tr + __popcll(msk & below);
-                    if (lane == C_TAIL + r) cv = tr + __popcll(msk);
-                }
-            }
-            if (ret) sh.ring[next][pos % POOL] = (uint16_t)slot;
-            const uint64_t md = __ballot(lane < n && next == R_DONE);
-            if (lane == C_DONE) cv += __popcll(md);
-            if (lane <= C_DONE) sh.ctl[lane] = cv;  /* tails, heads (unchanged), done */
-        }
-        /* keep the unit ring stocked: the queue atomic's latency is paid here once per 128 units
-         * instead of in every stage-A round (all waves on the chip contend for that address) */
-        if (!__builtin_amdgcn_readlane(cv, C_EXH) &&
-            __builtin_amdgcn_readlane(cv, C_UTAIL) - __builtin_amdgcn_readfirstlane(lds_peek(&sh.ctl[C_UHEAD])) < UREFILL) {
-            unsigned base = 0;
-            if (lane == 0) base = atomicAdd(P.queue, (unsigned)UREFILL);
-            base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
-            const unsigned left = base < P.nunits ? P.nunits - base : 0u;
-            const int nv = (int)(left < (unsigned)UREFILL ? left : (unsigned)UREFILL);
-            const int t0 = __builtin_amdgcn_readlane(cv, C_UTAIL);
-            for (int j = lane; j < nv; j += 64) sh.uring[(t0 + j) % URING] = base + (unsigned)j;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) {
-                __hip_atomic_store(&sh.ctl[C_UTAIL], t0 + nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (left <= (unsigned)UREFILL)
-                    __hip_atomic_store(&sh.ctl[C_EXH], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-        const int done = __builtin_amdgcn_readlane(cv, C_DONE);
-        int st = 0, best = -1;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int c = __builtin_amdgcn_readlane(cv, C_TAIL + r) - __builtin_amdgcn_readlane(cv, C_HEAD + r);
-            if (c > best) {
-                best = c;
-                st = r;
-            }
-        }
-        const int take = min(64, best);
-        if (take > 0) {
-            const int h0 = __builtin_amdgcn_readlane(cv, C_HEAD + st);
-            if (lane < take) slot = sh.ring[st][(h0 + lane) % POOL];
-            if (lane == 0) sh.ctl[C_HEAD + st] = h0 + take;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&sh.serving, ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(0);
-        n = take;
-        if (done == POOL) break;
-        if (take == 0) {
-            ++st_idle;
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-#endif
         if (dbg) {  /* debug only; compile-time indices keep the counters in registers */
 #pragma unroll
             for (int r = 0; r < NR; ++r)
@@ -862,9 +663,8 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         const bool active = lane < n;
         Task t;
         const int stage = st == R_A ? 0 : st < R_M ? 1 : 2;
-#if VPT_ONE_A
         /* one copy of stage A in the code: a batch of ring A runs it alone, a batch of an S/M ring
-         * runs its event first and then stage A on the same lanes (VPT_FUSE_A) */
+         * runs its event first and then stage A on the same lanes */
         SECT_BEGIN(ld);
         if (active) load_task(sh, slot, t, true);
         else {
@@ -882,40 +682,6 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         SECT_BEGIN(stt);
         if (active) store_task(sh, slot, t, true);
         SECT_END(stt, SECT_STORE);
-#else
-        if (stage == 0) {
-            if (active) load_task(sh, slot, t, true);
-            else {
-                t.c1 = 0;
-                t.in_path = false;
-                t.killed = false;
-            }
-            next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
-            if (active) store_task(sh, slot, t, true);
-        } else {
-            if (active) {
-                load_task(sh, slot, t, VPT_FUSE_A != 0 && !VPT_LATE_UNIT);
-                smp.X = t.X;
-                run_event<EST, COUNT>(S, smp, t, m, st);
-                t.X = smp.X;
-            } else {
-                t.c1 = 0;
-                t.in_path = false;
-                t.killed = false;
-            }
-#if VPT_FUSE_A
-            /* every task leaving S/M goes to stage A: the same wave runs it on the same lanes
-             * right away, instead of storing the batch, returning it to ring A under the lock and
-             * loading it again in another wave */
-            if (VPT_LATE_UNIT && active) load_task_unit(sh, slot, t);  /* not live across S/M */
-            next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
-            if (active) store_task(sh, slot, t, true);
-#else
-            if (active) store_task(sh, slot, t, false);
-            next = R_A;
-#endif
-        }
-#endif
         if (dbg) {
             const unsigned long long now = dbg_clock(dbg);
 #pragma unroll

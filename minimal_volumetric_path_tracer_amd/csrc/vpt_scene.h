@@ -39,5 +39,6 @@ struct DevScene {
     GeoSphere geo[VPT_MAX_SPHERES];
     vpt_sphere sph[VPT_MAX_SPHERES];
 };
+static_assert(VPT_MAX_SPHERES <= 64, "DevScene's per-sphere bit masks (1ull << i) hold at most 64 spheres");
 
 #endif

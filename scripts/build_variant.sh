@@ -8,9 +8,14 @@ name=$1
 shift
 mkdir -p build_variants
 C=minimal_volumetric_path_tracer_amd/csrc
-flock /tmp/vpt_build_variant.lock make -s -C "$C" vpt_host.o vpt_multi.o vpt_build_id.o
-/opt/rocm/bin/hipcc --offload-arch=${VARCH:-gfx950} -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
-    -Wno-unused-function "$@" -c "$C/vpt_kernels.hip" -o "build_variants/vpt_kernels_$name.o"
-/opt/rocm/bin/hipcc --offload-arch=${VARCH:-gfx950} -shared -fPIC "build_variants/vpt_kernels_$name.o" "$C/vpt_host.o" "$C/vpt_multi.o" "$C/vpt_build_id.o" \
+flock /tmp/vpt_build_variant.lock make -s -C "$C" vpt_host.o vpt_multi.o
+FLAGS="--offload-arch=${VARCH:-gfx950} -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function $*"
+/opt/rocm/bin/hipcc $FLAGS -c "$C/vpt_kernels.hip" -o "build_variants/vpt_kernels_$name.o"
+# the variant's own build id (sources + its flags + its name), so a result measured on a variant is
+# never recorded under the production library's id
+VID=$(python3 scripts/build_id.py "variant:$name | $FLAGS")
+echo "const char* vpt_build_id(void) { return \"$VID\"; }" > "build_variants/vpt_build_id_$name.c"
+cc -O2 -fPIC -c "build_variants/vpt_build_id_$name.c" -o "build_variants/vpt_build_id_$name.o"
+/opt/rocm/bin/hipcc --offload-arch=${VARCH:-gfx950} -shared -fPIC "build_variants/vpt_kernels_$name.o" "$C/vpt_host.o" "$C/vpt_multi.o" "build_variants/vpt_build_id_$name.o" \
     -o "build_variants/libvpt_$name.so" -lpthread -L/opt/rocm/lib -lrccl
 echo "build_variants/libvpt_$name.so"

@@ -76,7 +76,7 @@ def prims():
 @pytest.fixture(scope="session", params=["libm", "portable"])
 def orc(request):
     """both oracle builds: libm (glibc calls) and portable (csrc/vpt_math.h lm_*, the HIP kernel's
-    arithmetic).  With VPT_GLIBC_MATH=1 the two are the same function bit for bit, so every
+    arithmetic: glibc's algorithms restated).  The two are the same function bit for bit, so every
     reference bar holds for the arithmetic the GPU executes."""
     from oracle.oracle import Oracle
 

@@ -7,6 +7,7 @@ Bars (DESIGN.md, Parity):
     and green/blue channels within 1e-9 relative for >= 99 % of samples; the red channel differs
     only through the reference's rounding-coin-flip hazards, checked statistically.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -15,6 +16,7 @@ from conftest import GOLDEN, bitwise_equal
 from scenes import SCENES
 
 import minimal_volumetric_path_tracer_amd as vpt
+from minimal_volumetric_path_tracer_amd import _lib
 
 pytestmark = pytest.mark.gpu
 SEED = 0x5EED0001
@@ -441,6 +443,79 @@ def test_config1_full_size_256spp_vs_oracle(gpu_tracer, orc_vm):
         row = orc_vm.render(1024, 1024, 256, 0, seed=SEED, y0=y, y1=y + 1, threads=8)[fr]
         assert bitwise_equal(img[fr], row).all(), fr
     assert img.max() > 0
+
+
+@pytest.mark.gpu
+def test_config2_full_size_mis_hg_1024spp_vs_oracle(gpu_tracer, orc_vm):
+    """BASELINE configs[2] -- the north-star workload -- at its own size: MIS (free flight +
+    equi-angular, MISVPTTracerRecursive, include/vptShadeMethods.h:1345-1481) with HG g = 0.5,
+    1024 x 1024 x 1024 spp, the auto layout at 1024 spp (30 x 32 samples, then the 64-sample taper:
+    40 chunks), the pool at full occupancy.  Six file rows are recomputed by the oracle's pixel loop
+    (src/rt.cpp:784-800, ~6 M CPU samples) bit for bit; the whole image is finite."""
+    sc = SCENES["default"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    img = gpu_tracer.render(width=1024, height=1024, spp=1024, estimator="mis", hg_g=0.5, seed=SEED, fp64=True)
+    assert img.shape == (1024, 1024, 3) and np.isfinite(img).all() and img.max() > 0
+    for fr in (0, 187, 511, 640, 888, 1023):
+        y = 1023 - fr
+        row = orc_vm.render(1024, 1024, 1024, 1, hg_g=0.5, seed=SEED, y0=y, y1=y + 1, threads=16)[fr]
+        assert bitwise_equal(img[fr], row).all(), fr
+
+
+@pytest.mark.gpu
+def test_config3_full_size_dense_depth8_4096spp_vs_oracle(gpu_tracer, orc_vm):
+    """BASELINE configs[3] at its own size: free flight in the dense medium (sigma_t 0.03), paths capped
+    at 8 vertices, 2048 x 2048 x 4096 spp (126 x 32-sample chunks + the taper: 136 chunks, 13.7 GB
+    of partials).  Two file rows (~17 M CPU samples) recomputed by the oracle bit for bit; the whole
+    image is finite and lit."""
+    sc = SCENES["default"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    kw = dict(sigma_a=0.003, sigma_s=0.027, max_depth=8)
+    img = gpu_tracer.render(width=2048, height=2048, spp=4096, estimator="ff", seed=SEED, fp64=True, **kw)
+    assert img.shape == (2048, 2048, 3) and np.isfinite(img).all() and img.max() > 0
+    for fr in (5, 1400):
+        y = 2047 - fr
+        row = orc_vm.render(2048, 2048, 4096, 0, seed=SEED, y0=y, y1=y + 1, threads=16, **kw)[fr]
+        assert bitwise_equal(img[fr], row).all(), fr
+
+
+def _set_launch_bound(tracer, log2):
+    f = vpt.lib().vpt_debug_set_launch_bound
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    _lib.check(f(tracer._ctx, log2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,spp,log2,est,kw", [
+    # 7 launches of 1664 units, the last one 1280 (tests/test_launch_plan.py)
+    (32, 32, 96, 12, "ff", {}),
+    (32, 32, 96, 12, "mis", dict(hg_g=0.5)),
+    # configs[4]'s layout: 8192 spp -> 64-sample chunks + taper (137 chunks), split into 4 launches
+    (8, 6, 8192, 14, "mis", {}),
+])
+def test_split_launches_equal_one_launch(gpu_tracer, orc_vm, w, h, spp, log2, est, kw):
+    """The multi-launch path that BASELINE configs[4] takes on every GPU (2^34 samples per GPU > the
+    2^26-samples-per-workgroup launch bound): the same render with the bound lowered
+    (vpt_debug_set_launch_bound) so that it takes several launches, the last partial, equals the
+    one-launch render and the oracle bit for bit (src/rt.cpp:786-800: every sample once, in order)."""
+    sc = SCENES["default"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    cfg = dict(width=w, height=h, spp=spp, estimator=est, seed=SEED + 5, fp64=True, **kw)
+    one = gpu_tracer.render(**cfg)
+    _set_launch_bound(gpu_tracer, log2)
+    try:
+        split = gpu_tracer.render(**cfg)
+    finally:
+        _set_launch_bound(gpu_tracer, 26)
+    assert bitwise_equal(split, one).all()
+    ref = orc_vm.render(w, h, spp, {"ff": 0, "mis": 1}[est], seed=SEED + 5, threads=16, **kw)
+    assert bitwise_equal(split, ref).all()
+    with pytest.raises(vpt.VPTError):
+        _set_launch_bound(gpu_tracer, 27)
 
 
 # ---------------------------------------------------------------- estimators 2-4 (SURVEY 8f rank 2)
