@@ -269,20 +269,63 @@ def cpu_baseline(img: np.ndarray, c: dict, threads: int) -> dict:
     return res
 
 
-def pmc_profile(config: str, world: int):
+PMC_FILES = {"ff": "pmc_pool_kernel.json", "mis": "pmc_pool_kernel_mis.json"}
+
+
+def pmc_profile(config: str, world: int, build: str):
     """The committed rocprofv3 PMC summary of this same command for the dominant kernel
-    (profiles/<round>/pmc_pool_kernel.json, scripts/pmc.sh + scripts/pmc_summary.py), newest round
-    first.  Counters cannot be read live without the profiler; None when no profile matches."""
-    if config != "ff" or world != 1:
+    (profiles/<round>/pmc_pool_kernel[_mis].json, scripts/pmc.sh + scripts/pmc_summary.py), newest round
+    first -- used only when it was collected on THIS library (its build_id equals vpt.build_id()), so
+    the counters in the line belong to the code that ran.  Counters cannot be read live without the
+    profiler; None when no profile of this build exists."""
+    if config not in PMC_FILES or world != 1:
         return None
     import glob
 
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_pool_kernel.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", PMC_FILES[config])), reverse=True):
         try:
-            return json.load(open(f))
+            prof = json.load(open(f))
         except (OSError, ValueError):
             continue
+        if prof.get("build_id") == build:
+            prof["path"] = os.path.relpath(f, ROOT)
+            return prof
     return None
+
+
+def pmc_fields(prof, kern_ms: float, fb_bytes: int, partial_bytes: int) -> dict:
+    """north_star's 'rocprof-reported achieved HBM GB/s and VALU occupancy' (BASELINE.md:71-75) from the
+    build's own PMC profile: HBM GB/s = traffic / the kernel time measured in this run, SIMD VALU busy,
+    VALU lane use, and the traffic over the algorithmic bytes (the framebuffer the image needs; the
+    chunk partials the design writes on purpose).  Nulls without a profile of this build."""
+    t = pmc_traffic(prof)
+    der = (prof or {}).get("derived", {})
+    return {
+        "hbm_gbs": round(t / (kern_ms * 1e-3) / 1e9, 2) if t else None,
+        "valu_busy": round(der["simd_valu_busy_frac"], 4) if "simd_valu_busy_frac" in der else None,
+        "lane_util": round(der["valu_lane_utilization"], 4) if "valu_lane_utilization" in der else None,
+        "traffic_over_framebuffer": round(t / fb_bytes, 2) if t else None,
+        "traffic_over_partials": round(t / partial_bytes, 3) if t else None,
+        "pmc_profile": (prof or {}).get("path"),
+        "pmc_build_id": (prof or {}).get("build_id"),
+    }
+
+
+def fb_bytes(c: dict) -> int:
+    """the float32 framebuffer of one image (what the image itself needs written)"""
+    return c["width"] * c["height"] * 3 * 4
+
+
+def partial_bytes(c: dict) -> int:
+    """the chunk partials one launch writes (float64 RGB per pixel per chunk, csrc/vpt_chunks.h)"""
+    spp = c["spp"]
+    C = max(32, (spp + 127) // 128) if spp > 32 else spp
+    head = spp - min(spp, 2 * C) if spp > C else spp
+    n, rem = -(-head // C), spp - head
+    while rem > 0:
+        rem -= (rem + 2) // 3
+        n += 1
+    return c["width"] * c["height"] * 3 * 8 * n
 
 
 def pmc_traffic(prof):
@@ -440,7 +483,8 @@ def main() -> None:
     ns = None
     if args.config == "ff" and not args.no_north_star:
         ns = measure(CONFIGS[NORTH_STAR], args, tracers, streams, world, rank, dev)
-    prof = pmc_profile(args.config, world)
+    build = vpt.build_id()
+    prof = pmc_profile(args.config, world, build)
     full = pmc_fp64_flop(prof)
     kern_ms, T = m["kern_ms"], m["T"]
     if rank == 0:
@@ -475,6 +519,7 @@ def main() -> None:
                 "peak_no_fma": FP64_PEAK_TFLOPS / 2,
                 "frac_of_no_fma_peak": round(m["achieved"] / (FP64_PEAK_TFLOPS / 2), 5),
                 "traffic": pmc_traffic(prof),
+                **pmc_fields(prof, kern_ms, fb_bytes(c), partial_bytes(c)),
                 "kernel": (f"pool_kernel<{c['estimator']}> + reduce_kernel (one launch pair)"
                            if c["estimator"] not in ("ray_marching",) else "render_kernel_simple (one lane per pixel)"),
                 "kernel_ms": round(kern_ms, 3),
@@ -488,11 +533,13 @@ def main() -> None:
                 "note": "FP64 VALU bound (no dense contraction exists, no MFMA): peak 78.6 TFLOP/s counts an FMA as "
                         "2 flop; the path runs with contraction off (the reference's rounding), so 39.3 TFLOP/s "
                         "(peak_no_fma) is the ceiling for its separately rounded mul/add. achieved/frac count "
-                        "intersection flops only (SURVEY 8d); all_fp64_* count every FP64 VALU op of the kernel "
-                        "(committed PMC profile of this command, profiles/r*/pmc_pool_kernel.json)",
+                        "intersection flops only (SURVEY 8d); all_fp64_*, traffic, hbm_gbs, valu_busy and lane_util "
+                        "come from the committed PMC profile of this command collected on this build "
+                        "(pmc_profile, pmc_build_id == build_id; null when none exists); traffic_over_* divide "
+                        "the HBM bytes by the float32 framebuffer and by the chunk partials the design writes",
             },
             "image_mean": [round(float(x), 6) for x in img.reshape(-1, 3).mean(0)],
-            "build_id": vpt.build_id(),
+            "build_id": build,
         }
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         if world == 1 and not args.no_cpu:
@@ -512,6 +559,8 @@ def main() -> None:
                  "kernel_ms": round(ns["kern_ms"], 3),
                  "tests_per_sample": round(ns["T"], 3),
                  "roofline_frac": round(ns["achieved"] / FP64_PEAK_TFLOPS, 5),
+                 "pmc": pmc_fields(pmc_profile(NORTH_STAR, world, build), ns["kern_ms"], fb_bytes(cn),
+                                   partial_bytes(cn)),
                  "image_mean": [round(float(x), 6) for x in ns["image"].reshape(-1, 3).mean(0)]}
             cb = res.get("cpu_baseline")
             if cb:

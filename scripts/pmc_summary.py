@@ -2,6 +2,9 @@
 
     python scripts/pmc_summary.py gpurun_out/pmc_r01 'pool_kernel<0, false>' > profiles/r01/pmc_pool_kernel.json
 
+Records the build id the passes ran (from bench.py's JSON line in each pass's log); bench.py uses the
+profile only for the library with that id.
+
 Takes, in every pass, the LAST dispatch whose kernel name contains the pattern (bench.py runs the
 counting build first, then the timed launch), and derives lane utilisation, wait fractions and HBM
 bytes.  gfx950: FETCH_SIZE counts half of a streamed read, so HBM reads = 2 * FETCH_SIZE KiB
@@ -30,6 +33,22 @@ def last_dispatch(path, pattern):
             "agpr": r0["Accum_VGPR_Count"], "sgpr": r0["SGPR_Count"],
             "duration_ns": int(r0["End_Timestamp"]) - int(r0["Start_Timestamp"])}
     return info, counters
+
+
+def build_id_of(d):
+    """the library build every pass ran (bench.py's JSON line prints vpt.build_id()); the passes must agree,
+    so bench.py can tie the counters to the library it loads"""
+    ids = set()
+    for f in sorted(glob.glob(os.path.join(d, "p*.log"))):
+        for line in open(f):
+            if line.startswith("{"):
+                try:
+                    ids.add(json.loads(line).get("build_id"))
+                except ValueError:
+                    pass
+    if len(ids) != 1 or None in ids:
+        raise SystemExit(f"passes under {d} ran builds {sorted(map(str, ids))}: expected exactly one")
+    return ids.pop()
 
 
 def main():
@@ -79,7 +98,8 @@ def main():
     if g("SQ_LEVEL_WAVES") and g("SQ_BUSY_CYCLES"):
         der["mean_resident_waves_per_se"] = g("SQ_LEVEL_WAVES") / g("SQ_BUSY_CYCLES")
     out = {"source": f"rocprofv3 --pmc <counters> --kernel-trace, one pass per counter group (scripts/pmc.sh), "
-                     f"{os.path.basename(d)}", "dispatch": dispatch, "counters": c, "derived": der}
+                     f"{os.path.basename(d)}", "build_id": build_id_of(d), "dispatch": dispatch, "counters": c,
+           "derived": der}
     print(json.dumps(out, indent=1))
 
 

@@ -7,13 +7,40 @@ import minimal_volumetric_path_tracer_amd as vpt
 from oracle.oracle import Oracle
 
 
-def test_committed_pmc_profile_is_read():
-    p = bench.pmc_profile("ff", 1)
-    assert p is not None and "pool_kernel<0, false>" in p["dispatch"]["kernel"]
+def test_pmc_profile_only_for_its_build(tmp_path, monkeypatch):
+    """a PMC profile is quoted only by the library build it was collected on (profiles/r*/pmc_*.json
+    carry build_id, scripts/pmc_summary.py); newest round first"""
+    import json
+    import os
+
+    base = json.load(open(os.path.join(bench.ROOT, "profiles", "r03", "pmc_pool_kernel.json")))
+    for rnd, bid in (("r98", "aaaa"), ("r99", "bbbb")):
+        os.makedirs(tmp_path / "profiles" / rnd)
+        json.dump(dict(base, build_id=bid), open(tmp_path / "profiles" / rnd / "pmc_pool_kernel.json", "w"))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    p = bench.pmc_profile("ff", 1, "aaaa")
+    assert p is not None and p["build_id"] == "aaaa" and p["path"] == os.path.join("profiles", "r98", "pmc_pool_kernel.json")
+    assert bench.pmc_profile("ff", 1, "cccc") is None
+    assert bench.pmc_profile("mis", 1, "aaaa") is None and bench.pmc_profile("ff", 2, "aaaa") is None
     t = bench.pmc_traffic(p)
     assert t == int((2 * p["counters"]["FETCH_SIZE"] + p["counters"]["WRITE_SIZE"]) * 1024) and t > 0
     assert bench.pmc_fp64_flop(p) > 0
-    assert bench.pmc_profile("mis", 1) is None and bench.pmc_profile("ff", 2) is None
+    c = bench.CONFIGS["ff"]
+    f = bench.pmc_fields(p, 50.0, bench.fb_bytes(c), bench.partial_bytes(c))
+    assert abs(f["hbm_gbs"] - t / 0.05 / 1e9) < 0.01 and 0 < f["valu_busy"] < 1 and 0 < f["lane_util"] < 1
+    assert bench.fb_bytes(c) == 1024 * 1024 * 12 and bench.partial_bytes(c) == 1024 * 1024 * 24 * 16
+    assert f["traffic_over_partials"] == round(t / bench.partial_bytes(c), 3) and f["pmc_build_id"] == "aaaa"
+    assert all(v is None for v in bench.pmc_fields(None, 50.0, 1, 1).values())
+
+
+def test_partial_bytes_match_the_chunk_layout():
+    """bench's partial byte count uses the auto layout of csrc/vpt_chunks.h (via the C library's plan)"""
+    import test_launch_plan as tlp
+
+    for cfg in bench.CONFIGS.values():
+        units, _ = tlp.units_of(cfg["width"], cfg["height"], cfg["spp"])
+        tiles = ((cfg["width"] + 7) // 8) * ((cfg["height"] + 7) // 8) * 64
+        assert bench.partial_bytes(cfg) == cfg["width"] * cfg["height"] * 24 * (units // tiles)
 
 
 def test_cpu_port_check_rmse():
