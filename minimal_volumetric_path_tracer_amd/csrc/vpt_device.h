@@ -1025,10 +1025,33 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
  * H5: 80-87 % of point-light events).  The shadow ray draws nothing, so it is cast after the cone
  * ray here and only when its result survives: same draws, same bits, one ray cast fewer in most
  * point-light medium events (counting mode still adds its tests). */
-template <bool COUNT, int LT = -1>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
+/* the shadow ray toward a point light and its radiance, volumetricBasicFunctions.h:295-304 / :236-245
+ * (single_scattering's point-light branch) */
+template <bool COUNT>
+VPT_DEV dv3 point_shadow_ld(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
+                            double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource)
+{
+    const dv3 lp = sph_p(S, src);
+    const dv3 rad = sph_rad(S, src);
+    dv3 Ld = mk(0, 0, 0);
+    if (visibility(S, smp, lp, xt, false, -1.0, false)) {
+        double distanceLight = dot(sub(lp, xt), sub(lp, xt));
+        dv3 Le = scl(rad, (1 / distanceLight));
+        double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, nrm(sub(lp, xt)));
+        dv3 Ls = scl(scl(Le, transmitance(xt, lp, sigma_t)), ph);
+        if (with_sigma) Ld = scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
+        else Ld = scl(Ls, (1 / probSource));
+    }
+    return Ld;
+}
+
+/* DS (defer shadow, the pool kernel's point-light medium rings): a lane whose cone ray misses the
+ * point light does not cast the shadow ray here -- it sets `pending` and returns 0; the pool runs
+ * point_shadow_ld for such lanes later, 64 at a time (ring R_SH) */
+template <bool COUNT, int LT = -1, bool DS = false>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
 VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
                               double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource,
-                              bool zero_ok = false)
+                              bool zero_ok = false, bool* pending = nullptr)
 {
     const double lr = LT == 1 ? 0.0 : S->sph[src].r;
     const dv3 lp = sph_p(S, src);
@@ -1064,16 +1087,13 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
             else Ld = scl(scl(Ls, (1 / prob_wl)), (1 / probSource));
         }
     } else if (point) {
-        SECT_BEGIN(swi);
-        if (visibility(S, smp, lp, xt, false, -1.0, false)) {
-            double distanceLight = dot(sub(lp, xt), sub(lp, xt));
-            dv3 Le = scl(rad, (1 / distanceLight));
-            double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, nrm(sub(lp, xt)));
-            dv3 Ls = scl(scl(Le, transmitance(xt, lp, sigma_t)), ph);
-            if (with_sigma) Ld = scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
-            else Ld = scl(Ls, (1 / probSource));
+        if (DS) {
+            *pending = true;
+        } else {
+            SECT_BEGIN(swi);
+            Ld = point_shadow_ld(S, smp, xt, din, src, sigma_t, with_sigma, sigma_s, trxt, probSource);
+            SECT_END(swi, SECT_M_SHADOW_IN);
         }
-        SECT_END(swi, SECT_M_SHADOW_IN);
     }
     SECT_END(sw, SECT_M_SS_SHADOW);
     return Ld;
@@ -1227,10 +1247,12 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
     return EV_SURF;
 }
 
-/* surface event: point-light NEE (pLight), sphere-light MIS (MISv2), BSDF continuation (bdsf) */
+/* surface event: point-light NEE (pLight), sphere-light MIS (MISv2), BSDF continuation (bdsf).
+ * cont = false: the path ends at the next roulette draw (the pool's kill prediction), so only the
+ * radiance is updated -- the continuation's draws, direction and throughput are never read. */
 template <int EST, bool COUNT, int MK = -1, int PT = -1>  /* MK: material, PT: point light (1), if known */
 VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
-                           const Medium& m)
+                           const Medium& m, bool cont = true)
 {
     const double sigma_t = m.sigma_a + m.sigma_s;
     const double continueprob = 0.6;
@@ -1281,17 +1303,20 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
                                       : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
     SECT_END(mis, SECT_S_MIS);
     SECT_BEGIN(bd);
-    dv3 wi = mk(0, 0, 0);
-    double pdf = 0;
-    dv3 fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
-    wi = nrm(wi);
-    double cosine = dot(nx, wi);
+    /* (the radiance update reads the throughput before bdsf's update, as in the reference) */
     if (EST == 0) p.L = add(p.L, scl(mul(add(Ldp, Ld), p.beta), (1 / continueprob)));
     else p.L = add(p.L, mul(p.beta, scl(add(Ldp, Ld), (1 / continueprob))));
-    p.beta = scl(scl(scl(mul(p.beta, fs), (1 / continueprob)), cosine), (1 / pdf));
-    p.o = xs;
-    p.d = wi;
-    p.depth++;
+    if (cont) {
+        dv3 wi = mk(0, 0, 0);
+        double pdf = 0;
+        dv3 fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
+        wi = nrm(wi);
+        double cosine = dot(nx, wi);
+        p.beta = scl(scl(scl(mul(p.beta, fs), (1 / continueprob)), cosine), (1 / pdf));
+        p.o = xs;
+        p.d = wi;
+        p.depth++;
+    }
     SECT_END(bd, SECT_S_BDSF);
 }
 
@@ -1347,9 +1372,50 @@ VPT_DEV void eqa_medium(const DevScene* __restrict__ S, const Path& p, const Eve
     pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
 }
 
-template <int EST, bool COUNT, int LT = -1>
+/* the medium event after single scattering's Ld (vptShadeMethods.h:1318-1332 / :1461-1477): the
+ * radiance update, then -- unless the path ends at the next roulette draw (cont = false) -- the phase
+ * sample and the throughput.  T: transmittance to xt, pdf: the equi-angular pdf (estimators 1, 4). */
+template <int EST, bool COUNT>
+VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double pdf, dv3 xt, const Medium& m, bool cont)
+{
+    const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
+    const double sigma_t = sigma_a + sigma_s;
+    const double continueprob = 0.6;
+    if (EST == 0) {
+        p.L = add(p.L, scl(scl(mul(Ld, p.beta), (sigma_s / sigma_t)), (1 / continueprob)));
+        if (!cont) return;
+        SECT_BEGIN(ph);
+        dv3 wi = phase_sample(smp, p.d);
+        SECT_END(ph, SECT_M_PHASE);
+        p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
+        p.d = wi;
+    } else if (EST == 2) {  /* vptShadeMethods.h:1252-1258 */
+        p.L = add(p.L, mul(p.beta, scl(scl(Ld, (sigma_s / sigma_t)), (1 / continueprob))));
+        if (!cont) return;
+        dv3 wi = phase_sample(smp, p.d);
+        p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
+        p.d = wi;
+    } else {
+        p.L = add(p.L, mul(p.beta, scl(scl(Ld, (1 / pdf)), (1 / continueprob))));
+        if (!cont) return;
+        SECT_BEGIN(ph);
+        dv3 wi = phase_sample(smp, p.d);
+        SECT_END(ph, SECT_M_PHASE);
+        p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / pdf));
+        p.d = wi;
+    }
+    p.o = xt;
+    p.depth++;
+}
+
+/* medium event: single-scattering NEE toward the picked light, phase-function continuation.
+ * LT: 1 point light, 0 not, -1 unknown (the pool kernel's medium rings are keyed by it).  cont = false:
+ * radiance only (surface_event).  DS: a lane whose point-light shadow ray is deferred (single_scattering)
+ * stops after the light cone with *pending set, the scatter point in p.o and T, pdf in *eout (t, pdf);
+ * medium_shadow_event finishes it. */
+template <int EST, bool COUNT, int LT = -1, bool DS = false>
 VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e0,
-                          const Medium& m)
+                          const Medium& m, bool cont = true, Event* eout = nullptr, bool* pending = nullptr)
 {
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
@@ -1373,38 +1439,42 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
      * finite (p.L is never -0: it starts at +0 and only adds) -- single_scattering's H5 shortcut */
     const bool zero_ok = p.beta.x - p.beta.x == 0 && p.beta.y - p.beta.y == 0 && p.beta.z - p.beta.z == 0 &&
                          (!(EST == 1 || EST == 4) || (1 / e.pdf) - (1 / e.pdf) == 0);
-    if (EST == 0) {
-        SECT_BEGIN(ss);
-        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource, zero_ok);
-        SECT_END(ss, SECT_M_SS);
-        SECT_BEGIN(ph);
-        dv3 wi = phase_sample(smp, p.d);
-        SECT_END(ph, SECT_M_PHASE);
-        p.L = add(p.L, scl(scl(mul(Ld, p.beta), (sigma_s / sigma_t)), (1 / continueprob)));
-        p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
-        p.d = wi;
-    } else if (EST == 2) {  /* vptShadeMethods.h:1252-1258 */
-        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, false, sigma_s, 1.0, probSource, zero_ok);
-        dv3 wi = phase_sample(smp, p.d);
-        p.L = add(p.L, mul(p.beta, scl(scl(Ld, (sigma_s / sigma_t)), (1 / continueprob))));
-        p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
-        p.d = wi;
-    } else {
+    /* singleScattering (estimators 1, 4) weighs by the transmittance to xt; freeSingleScattering not */
+    constexpr bool ws = EST == 1 || EST == 4;
+    double T = 1.0;
+    if (ws) {
         SECT_BEGIN(tr);
-        double T = transmitance(p.o, xt, sigma_t);
+        T = transmitance(p.o, xt, sigma_t);
         SECT_END(tr, SECT_M_TR);
-        SECT_BEGIN(ss);
-        dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, true, sigma_s, T, probSource, zero_ok);
-        SECT_END(ss, SECT_M_SS);
-        SECT_BEGIN(ph);
-        dv3 wi = phase_sample(smp, p.d);
-        SECT_END(ph, SECT_M_PHASE);
-        p.L = add(p.L, mul(p.beta, scl(scl(Ld, (1 / e.pdf)), (1 / continueprob))));
-        p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / e.pdf));
-        p.d = wi;
     }
-    p.o = xt;
-    p.depth++;
+    SECT_BEGIN(ss);
+    bool pend = false;
+    dv3 Ld = single_scattering<COUNT, LT, DS>(S, smp, xt, p.d, e.src, sigma_t, ws, sigma_s, T, probSource, zero_ok, &pend);
+    SECT_END(ss, SECT_M_SS);
+    if (DS && pend) {
+        p.o = xt;
+        eout->t = T;
+        eout->pdf = e.pdf;
+        *pending = true;
+        return;
+    }
+    medium_tail<EST, COUNT>(smp, p, Ld, T, e.pdf, xt, m, cont);
+}
+
+/* the rest of a point-light medium event whose shadow ray was deferred (medium_event DS): the shadow
+ * ray from the light toward the scatter point p.o, its Ld, then medium_tail -- the operations and
+ * draws of the undivided event */
+template <int EST, bool COUNT>
+VPT_DEV void medium_shadow_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
+                                 const Medium& m, bool cont)
+{
+    const double sigma_t = m.sigma_a + m.sigma_s;
+    constexpr bool ws = EST == 1 || EST == 4;
+    const double T = ws ? e.t : 1.0;
+    SECT_BEGIN(swi);
+    const dv3 Ld = point_shadow_ld(S, smp, p.o, p.d, e.src, sigma_t, ws, m.sigma_s, T, 1.0 / S->n_emit);
+    SECT_END(swi, SECT_M_SHADOW_IN);
+    medium_tail<EST, COUNT>(smp, p, Ld, T, e.pdf, p.o, m, cont);
 }
 
 /* iterativePathTracer, include/shadeMethods.h:104-163 (estimator 5): surface-only path tracing.

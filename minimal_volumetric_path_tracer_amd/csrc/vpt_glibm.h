@@ -501,6 +501,82 @@ VM_QUAL double gm_atan2(double y, double x)
     return r;
 }
 
+/* ------------------------------------------------------------------ tan (s_tan.c)
+ * glibc 2.35's __tan, FMA build, for |x| <= 25 (the equi-angular sampler's angle lies in
+ * (-pi/2, pi/2), include/volumetricBasicFunctions.h:221): x itself below 0x1.b096cp-27; an odd
+ * polynomial up to 0.0608; around a node of the library's table (xi, fi, gi per 1/256, gl_tab) up to
+ * 0.787; above, x - n pi/2 as a + da (three pieces of pi/2) and, by the parity of n, tan or -1/tan of
+ * it -- by the same polynomial (-1/tan with glibc's double-double division) or around a table node.
+ * The forms are evaluated straight-line and selected (the polynomial and the table form once each,
+ * on the argument of the lane's range); |x| > 25, inf and NaN go to the translated gl_tan. */
+VM_TABLE(gm_tan_tab, {
+    0x1.2385a3cf2e4eap-7, 0x1.664ed49cfc666p-6, 0x1.ba1ba1cdb8745p-5, 0x1.11111111107c6p-3,
+    0x1.5555555555555p-2,                                /* 0-4 the odd polynomial */
+    0x1.11112e0a6b45fp-3, 0x1.5555555554dbdp-2,          /* 5-6 the table form's polynomial */
+    0x1.45f306dc9c883p-1, 0x1.8p+52,                     /* 7-8 2/pi, toint */
+    0x1.921fb58000000p+0, -0x1.dde973c000000p-27, -0x1.cb3b399d747f2p-55,  /* 9-11 pi/2 in three pieces */
+    0x1.b096cp-27, 0x1.f212dp-5, 0x1.92f1ap-1, 25.0})     /* 12-15 range bounds */
+enum { GN_P0 = 0, GN_Q1 = 5, GN_Q0, GN_HPINV, GN_TOINT, GN_MP1, GN_MP2, GN_PP3, GN_TINY, GN_SMALL, GN_MID, GN_BIG };
+#define GM_TAN_T(i, j) vm_as_f64(gl_tab[(0xC15C0ull - GL_TAB_LO) / 8 + 4 * (i) + (j)])
+
+VM_QUAL double gm_tan(double x)
+{
+    vm_ct* K = vm_tab(gm_tan_tab);
+    const double ax = vm_fabs(x);
+    /* |x| in (0.787, 25]: a + da = x - n pi/2 */
+    const double t = gm_fma(x, VM_T(K, GN_HPINV), VM_T(K, GN_TOINT));
+    const double xn = t - VM_T(K, GN_TOINT);
+    const int odd = (int)(gm_lo(t) & 1u);
+    double a0 = gm_fnma(xn, VM_T(K, GN_MP1), x);
+    a0 = gm_fnma(xn, VM_T(K, GN_MP2), a0);
+    const double pp3 = VM_T(K, GN_PP3);
+    const double a = gm_fnma(xn, pp3, a0);
+    const double da = gm_fnma(xn, pp3, a0 - a);
+    const int inR = ax > VM_T(K, GN_MID);
+    const int neg = a < 0;
+    /* the polynomial form: tan(x) = fma(x^3, P, x) below 0.0608; above, y = a + fma(a^3, P, da), and
+     * for odd n -1/y with y's tail yy (glibc's EADD + DIV2) */
+    const double v = inR ? a : x;
+    const double v2 = v * v;
+    double p = gm_fma(v2, VM_T(K, GN_P0), VM_T(K, GN_P0 + 1));
+    p = gm_fma(v2, p, VM_T(K, GN_P0 + 2));
+    p = gm_fma(v2, p, VM_T(K, GN_P0 + 3));
+    p = gm_fma(v2, p, VM_T(K, GN_P0 + 4));
+    const double v3 = v * v2;
+    const double rP = gm_fma(v3, p, x);
+    const double c = gm_fma(v3, p, da);
+    const double y = a + c;
+    const double yy = vm_fabs(a) > vm_fabs(c) ? (a - y) + c : (c - y) + a;
+    const double r = 1.0 / y;
+    const double h = r * y;
+    const double e = gm_fma(r, y, -h);
+    double w = ((1.0 - h) - e) + 0.0;
+    w = gm_fnma(yy, r, w);
+    const double q = w / y;
+    const double s1 = r + q;
+    const double rPoly = odd ? -(((r - s1) + q) + s1) : y;
+    /* the table form around xi = (i + 16) / 256 -- (fi + gi) p / (gi - p) + fi, or for odd n
+     * gi - (fi + gi) p / (p + fi) -- on |x| (0.0608 < |x| <= 0.787) or |a| + sign(a) da */
+    const double u = inR ? (neg ? -a : a) : ax;
+    const double du = inR ? (neg ? -da : da) : 0.0;
+    const int todd = inR && odd;
+    const double sg = (inR ? neg : x < 0) ? -1.0 : 1.0;
+    const double ti = gm_fma(u, 256.0, -15.5);
+    const int i = ti > 0.0 ? (ti < 186.5 ? (int)ti : 186) : 0;  /* (lanes of the other forms: any node) */
+    const double z = (u - GM_TAN_T(i, 0)) + du;
+    const double z2 = z * z;
+    const double z3 = z * z2;
+    const double pz = gm_fma(z3, gm_fma(z2, VM_T(K, GN_Q1), VM_T(K, GN_Q0)), z);
+    const double fi = GM_TAN_T(i, 1), gi = GM_TAN_T(i, 2);
+    const double num = (fi + gi) * pz;
+    const double qt = num / (todd ? pz + fi : gi - pz);
+    const double rTab = todd ? (gi - qt) * -sg : (qt + fi) * sg;
+    const double small = VM_T(K, GN_SMALL);
+    double res = ax <= VM_T(K, GN_TINY) ? x : ax <= small ? rP : !inR ? rTab : u <= small ? rPoly : rTab;
+    if (GM_UNLIKELY(!(ax <= VM_T(K, GN_BIG)))) res = gl_tan(x);
+    return res;
+}
+
 /* Out-of-line entry points for the kernel.  The tracer's direction samplers call acos and four
  * sin/cos at ~10 sites per stage; inlined, each site carries its own copy (code size, and
  * registers held across the expansion).  On the device these are real calls, returning their

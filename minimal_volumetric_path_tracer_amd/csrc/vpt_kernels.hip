@@ -834,6 +834,7 @@ int vpt_set_scene(vpt_context* ctx, const vpt_sphere* s, int n)
         if (q.material == 3) h.n_mat3++;
     }
     h.n_non3 = n - h.n_mat3;
+    vpt_erand48_jump(2 * h.n_mis + 5, &h.kp_sa, &h.kp_sc);
     HIP_OK(hipSetDevice(ctx->device));
     HIP_OK(hipMemcpy(ctx->d_scene, &h, sizeof h, hipMemcpyHostToDevice));
     ctx->h_scene = h;

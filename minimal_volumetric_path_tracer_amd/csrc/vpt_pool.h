@@ -45,8 +45,15 @@ namespace vpt {
 #ifndef VPT_POOL_WGS
 #define VPT_POOL_WGS 1      /* workgroups per CU (occupancy target; LDS and VGPR budgets follow) */
 #endif
-#ifndef VPT_POOL_SIZE
-#define VPT_POOL_SIZE 880
+/* Kill-predicting rings: a diffuse surface or medium event whose path the next roulette draw (or the
+ * depth cap) will end is known when decide() picks the event -- the draws in between are a fixed
+ * number (2 n_mis + 4 for a diffuse surface event: two per MIS light cone, the BSDF sample of MISv2
+ * and bdsf's cosine sample; 4 for a medium event: the light cone and the phase sample), and a dead
+ * path's stream is never read again (the next sample starts its own).  Such tasks wait in rings of
+ * their own, so their batches skip the continuation (bdsf / the phase sample, the throughput and ray
+ * updates) -- the same radiance, the same bits. */
+#ifndef VPT_KILL_RINGS
+#define VPT_KILL_RINGS 1
 #endif
 #ifndef VPT_SCHED_PRIO
 #define VPT_SCHED_PRIO 3    /* s_setprio level of the scheduler's critical section (0: off; A/B 3 vs 0: +0.7 %) */
@@ -65,10 +72,20 @@ namespace vpt {
  * 32 48.39 / 215.9; one round only (VPT_PREP_ROUNDS=1) 48.11 / 218.1 */
 #define VPT_PREP_MORE_MIN 24
 #endif
-constexpr int POOL = VPT_POOL_SIZE; /* task slots per workgroup: 182 B each + ~1.1 KB (161 KB at 880) */
+/* Deferred point-light shadow rays: a medium event toward a point light casts the shadow ray only when
+ * its light cone misses the light (13-20 % of them); such a batch ran that ray with ~8 of 64
+ * lanes (2.6 % of the kernel's wave-time, profiles/r03/sections_ff_prep.txt).  With this ring the lanes
+ * stop after the cone (scatter point, transmittance and pdf kept in the task) and a later batch casts
+ * 64 of those rays at once (medium_shadow_event) -- the same operations and draws. */
+#ifndef VPT_SHADOW_RING
+#define VPT_SHADOW_RING 0
+#endif
 constexpr int NF = 18;      /* doubles per task */
-constexpr int NR = 7;       /* rings */
-constexpr int R_A = 0, R_S = 1, R_M = 5, R_DONE = NR;
+/* rings: A; S diffuse x (sphere light, point light), metal, other; M (sphere light, point light);
+ * with VPT_KILL_RINGS the four diffuse-surface / medium rings again for tasks the event ends; with
+ * VPT_SHADOW_RING the deferred shadow rays */
+constexpr int R_A = 0, R_S = 1, R_M = 5, R_SD = 7, R_MD = 9, R_SH = VPT_KILL_RINGS ? 11 : 7;
+constexpr int NR = R_SH + (VPT_SHADOW_RING ? 1 : 0), R_DONE = NR;
 /* the scheduler's counters (TaskPool::ctl): ring tails, ring heads, slots retired, the unit ring's
  * tail, queue exhausted, refill in progress, the unit ring's head (one lane-parallel read fetches all) */
 constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_EXH = 2 * NR + 2, C_RFL = 2 * NR + 3,
@@ -79,6 +96,15 @@ static_assert(NCTL <= 64, "the counters are read lane-parallel by one wave");
 #endif
 constexpr int UREFILL = VPT_UREFILL, URING = 2 * UREFILL;  /* work-unit ring: one global queue atomic per UREFILL units */
 static_assert(URING >= 2 * UREFILL, "a refill (at most UREFILL entries from utail < uhead + UREFILL) must stay below uhead + URING");
+/* task slots per workgroup: as many as the CU's 160 KB of LDS hold beside the counters, the unit ring
+ * (and the debug build's section timers) -- 182 B each with 7 rings (880 slots), 190 B with 11 */
+#ifdef VPT_POOL_SIZE
+constexpr int POOL = VPT_POOL_SIZE;
+#else
+constexpr int POOL = NR == 7 ? 880
+                                     : (163840 - 4 * NCTL - 4 * URING - (VPT_SECTIONS ? 8 * 3 * SECT_USED * 4 : 0) - 64) /
+                                           (NF * 8 + 8 + 4 * 4 + 2 * NR);
+#endif
 
 /* debug statistics, in builds with -DVPT_POOL_DEBUG=1 (=2: top-level cycle split only, cheaper;
  * scripts/build_variant.sh) run with
@@ -110,7 +136,7 @@ struct TaskPool {
     uint32_t pix[POOL];      /* x | camera row << 16 of the unit's pixel */
     uint32_t c1[POOL];       /* one past the unit's last sample; 0 = no unit */
     uint32_t samp[POOL];     /* next sample to start | in_path << 31 */
-    uint32_t evw[POOL];      /* depth | id << 16 | src << 24 | killed << 31 */
+    uint32_t evw[POOL];      /* depth | id << 16 | src << 24 | shadow-dies << 30 | killed << 31 */
     uint16_t ring[NR][POOL]; /* slots waiting, per ring */
     /* the scheduler's counters, contiguous so that one lane-parallel LDS read fetches them all:
      * monotonic ring tails and heads, slots retired, the unit ring's tail, queue exhausted */
@@ -212,6 +238,8 @@ struct Task {
     unsigned c1;     /* one past the unit's last sample; 0 = the task needs a unit */
     unsigned i;      /* next sample to start */
     bool in_path, killed;
+    bool pend;       /* the event stopped for a deferred shadow ray (ring R_SH) */
+    bool sh_die;     /* ... and the path ends after it (the M ring was kill-predicted) */
 };
 
 /* the fields only stage A reads (unit, chunk sum, sample counter): loaded right before it */
@@ -237,7 +265,8 @@ __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bo
     const uint32_t ev = sh.evw[s];
     t.p.depth = (int)(ev & 0xFFFFu);
     t.e.id = (int)((ev >> 16) & 0xFFu);
-    t.e.src = (int)((ev >> 24) & 0x7Fu);
+    t.e.src = (int)((ev >> 24) & 0x3Fu);  /* (VPT_MAX_SPHERES <= 64) */
+    t.sh_die = ((ev >> 30) & 1u) != 0;
     t.killed = (ev >> 31) != 0;
     t.X = sh.X[s];
     if (full) load_task_unit(sh, s, t);
@@ -251,7 +280,7 @@ __device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, b
     sh.f[F_LX][s] = t.p.L.x; sh.f[F_LY][s] = t.p.L.y; sh.f[F_LZ][s] = t.p.L.z;
     sh.X[s] = t.X;
     sh.evw[s] = (uint32_t)(t.p.depth & 0xFFFF) | ((uint32_t)t.e.id << 16) | ((uint32_t)t.e.src << 24) |
-                (t.killed ? 0x80000000u : 0u);
+                (t.sh_die ? 0x40000000u : 0u) | (t.killed ? 0x80000000u : 0u);
     if (full) {
         sh.f[F_TD][s] = t.e.t;  /* stage_a leaves the distance the next stage reads in e.t */
         sh.f[F_KEY][s] = __longlong_as_double((long long)t.key);
@@ -288,25 +317,54 @@ __device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sample
         if (st == R_S + 2) t.killed = surface_event_pt<COUNT, 1>(S, smp, t.p, t.e);
         else if (st == R_S) t.killed = surface_event_pt<COUNT, 0>(S, smp, t.p, t.e);
         else t.killed = surface_event_pt<COUNT, -1>(S, smp, t.p, t.e);
+    } else if (VPT_SHADOW_RING && st == R_SH) {
+        /* the deferred point-light shadow rays, then the rest of their medium events */
+        SECT_BEGIN(ev);
+        medium_shadow_event<EST, COUNT>(S, smp, t.p, t.e, m, !t.sh_die);
+        SECT_END(ev, SECT_M_TOTAL);
+        t.killed = t.sh_die || !continue_path(smp, t.p, m);
     } else {
         SECT_BEGIN(ev);
+        /* a kill-predicted ring (R_SD.., R_MD..) runs its base ring's event without the continuation */
+        bool cont = true;
+        if (VPT_KILL_RINGS && st >= R_SD) {
+            cont = false;
+            st = st < R_MD ? st - R_SD + R_S : st - R_MD + R_M;
+        }
         /* metal (R_S + 2) and other materials (R_S + 3) are rare: 1.4 % of surface events at the
          * bench scene */
         if (st < R_M) {
-            if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m);
-            else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m);
+            if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m, cont);
+            else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m, cont);
             else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
             else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
         } else if (st == R_M) {
-            medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m);
+            medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m, cont);
         } else {
-            medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m);
+            medium_event<EST, COUNT, 1, VPT_SHADOW_RING != 0>(S, smp, t.p, t.e, m, cont, &t.e, &t.pend);
         }
         SECT_END(ev, st < R_M ? SECT_S_TOTAL : SECT_M_TOTAL);
+        if (VPT_SHADOW_RING && t.pend) {  /* the shadow ray and the roulette draw come in ring R_SH */
+            t.sh_die = !cont;
+            return;
+        }
         SECT_BEGIN(cp);
-        t.killed = !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
+        t.killed = !cont || !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
         SECT_END(cp, SECT_CONT);
     }
+}
+
+/* the kill prediction (VPT_KILL_RINGS): with the state X after decide(), does the roulette draw that
+ * follows the event -- `jump` draws on -- end the path, or does the depth cap (continue_path)? */
+template <int EST>
+__device__ __forceinline__ constexpr bool kill_predicted_est()
+{
+    return VPT_KILL_RINGS && (EST == 0 || EST == 1 || EST == 2 || EST == 4);
+}
+__device__ __forceinline__ bool path_ends_after_event(uint64_t X, int depth, const Medium& m, uint64_t ja, uint64_t jc)
+{
+    if (m.max_depth > 0 && depth + 1 >= m.max_depth) return true;
+    return vpt_erand48_value(vpt_erand48_skip(X, ja, jc)) < 1 - 0.6;
 }
 
 /* Stage A for the lanes with `active`: at most ONE decide() per task.  A converged preparation
@@ -481,11 +539,21 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         } else if (ev == EV_SURF) {  /* (the implicit estimator, EST 3, picks no light) */
             const int sk = sph_flag(S->m_skey1, t.e.id) | (sph_flag(S->m_skey2, t.e.id) << 1);
             result = R_S + (sk == 0 ? (EST == 3 || EST == 5 ? 0 : sph_flag(S->m_point, t.e.src)) : sk);
+            /* a diffuse surface event: 2 n_mis + 4 draws, then the roulette (S->kp_sa, kp_sc) */
+            if (kill_predicted_est<EST>() && !COUNT && sk == 0 &&
+                path_ends_after_event(t.X, t.p.depth, m, S->kp_sa, S->kp_sc))
+                result += R_SD - R_S;
         } else {
             result = R_M + (EST == 3 ? 0 : sph_flag(S->m_point, t.e.src));
             /* one slot (F_TD): stage M reads the sampled distance -- or, for the deferred
              * equi-angular estimators, tMax (with the draw in F_PDF) */
             if (!(EST == 1 || EST == 4)) t.e.t = t.e.dist;
+            /* a medium event: the light cone's two draws and the phase sample's two, then the roulette */
+            if constexpr (kill_predicted_est<EST>() && !COUNT) {
+                uint64_t ja, jc;
+                vpt_erand48_jump(5, &ja, &jc);
+                if (path_ends_after_event(t.X, t.p.depth, m, ja, jc)) result += R_MD - R_M;
+            }
         }
         SECT_END(dci, SECT_A_DECIDE_IN);
     }
@@ -673,12 +741,15 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             t.killed = false;
         }
         SECT_END(ld, SECT_LOAD);
+        t.pend = false;
         if (stage != 0 && active) {
             smp.X = t.X;
             run_event<EST, COUNT>(S, smp, t, m, st);
             t.X = smp.X;
         }
-        next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
+        /* a task whose event waits for its deferred shadow ray skips stage A and goes to ring R_SH */
+        next = stage_a<EST>(sh, P, S, m, smp, t, active && !(VPT_SHADOW_RING && t.pend), lane, below, dbga, D);
+        if (VPT_SHADOW_RING && t.pend) next = R_SH;
         SECT_BEGIN(stt);
         if (active) store_task(sh, slot, t, true);
         SECT_END(stt, SECT_STORE);
@@ -703,9 +774,10 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             atomicAdd(&stats[15], st_retry);
             atomicAdd(&stats[19], st_sched);
 #pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                atomicAdd(&stats[r], st_b[r]);
-                atomicAdd(&stats[7 + r], st_l[r]);
+            for (int r = 0; r < NR; ++r) {  /* (kill-predicted rings are counted with their base ring) */
+                const int rb = r < R_SD ? r : r < R_MD ? r - R_SD + R_S : r - R_MD + R_M;
+                atomicAdd(&stats[rb], st_b[r]);
+                atomicAdd(&stats[7 + rb], st_l[r]);
             }
 #pragma unroll
             for (int k = 0; k < 3; ++k) atomicAdd(&stats[16 + k], st_c[k]);

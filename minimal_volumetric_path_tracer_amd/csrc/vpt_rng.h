@@ -75,4 +75,18 @@ VPT_HD uint64_t vpt_erand48_skip3(uint64_t X)
     return (X * 0xD498BD0AC4B5ull + 0xAA8544E593Dull) & 0xFFFFFFFFFFFFull;
 }
 
+/* the n-draw jump X -> A X + C mod 2^48 (the recurrence composed n times) */
+VPT_HD void vpt_erand48_jump(int n, uint64_t* A, uint64_t* C)
+{
+    uint64_t a = 1, c = 0;
+    for (int k = 0; k < n; ++k) {
+        a = (a * 0x5DEECE66Dull) & 0xFFFFFFFFFFFFull;
+        c = (c * 0x5DEECE66Dull + 0xBull) & 0xFFFFFFFFFFFFull;
+    }
+    *A = a;
+    *C = c;
+}
+
+VPT_HD uint64_t vpt_erand48_skip(uint64_t X, uint64_t A, uint64_t C) { return (X * A + C) & 0xFFFFFFFFFFFFull; }
+
 #endif

@@ -33,7 +33,10 @@ struct DevScene {
     /* per-sphere flags as bit masks (bit i = sphere i; VPT_MAX_SPHERES <= 64), read with a per-lane id
      * by shifts of wave-uniform words instead of per-lane loads of GeoSphere fields */
     uint64_t m_emitter, m_point, m_mat3, m_skey1, m_skey2;  /* skey = m_skey1 bit + 2 * m_skey2 bit */
-    uint64_t pad2_[3];
+    /* erand48 jump (A, C) from the state after decide() to the roulette draw that follows a diffuse
+     * surface event: 2 n_mis + 4 draws of the event, then the roulette (the pool's kill prediction) */
+    uint64_t kp_sa, kp_sc;
+    uint64_t pad2_[1];
     int32_t emit[VPT_MAX_SPHERES];
     int32_t mis_light[VPT_MAX_SPHERES];
     GeoSphere geo[VPT_MAX_SPHERES];
