@@ -1045,13 +1045,10 @@ VPT_DEV dv3 point_shadow_ld(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
     return Ld;
 }
 
-/* DS (defer shadow, the pool kernel's point-light medium rings): a lane whose cone ray misses the
- * point light does not cast the shadow ray here -- it sets `pending` and returns 0; the pool runs
- * point_shadow_ld for such lanes later, 64 at a time (ring R_SH) */
-template <bool COUNT, int LT = -1, bool DS = false>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
+template <bool COUNT, int LT = -1>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
 VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
                               double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource,
-                              bool zero_ok = false, bool* pending = nullptr)
+                              bool zero_ok = false)
 {
     const double lr = LT == 1 ? 0.0 : S->sph[src].r;
     const dv3 lp = sph_p(S, src);
@@ -1087,13 +1084,9 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
             else Ld = scl(scl(Ls, (1 / prob_wl)), (1 / probSource));
         }
     } else if (point) {
-        if (DS) {
-            *pending = true;
-        } else {
-            SECT_BEGIN(swi);
-            Ld = point_shadow_ld(S, smp, xt, din, src, sigma_t, with_sigma, sigma_s, trxt, probSource);
-            SECT_END(swi, SECT_M_SHADOW_IN);
-        }
+        SECT_BEGIN(swi);
+        Ld = point_shadow_ld(S, smp, xt, din, src, sigma_t, with_sigma, sigma_s, trxt, probSource);
+        SECT_END(swi, SECT_M_SHADOW_IN);
     }
     SECT_END(sw, SECT_M_SS_SHADOW);
     return Ld;
@@ -1410,12 +1403,10 @@ VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double 
 
 /* medium event: single-scattering NEE toward the picked light, phase-function continuation.
  * LT: 1 point light, 0 not, -1 unknown (the pool kernel's medium rings are keyed by it).  cont = false:
- * radiance only (surface_event).  DS: a lane whose point-light shadow ray is deferred (single_scattering)
- * stops after the light cone with *pending set, the scatter point in p.o and T, pdf in *eout (t, pdf);
- * medium_shadow_event finishes it. */
-template <int EST, bool COUNT, int LT = -1, bool DS = false>
+ * radiance only (surface_event). */
+template <int EST, bool COUNT, int LT = -1>
 VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e0,
-                          const Medium& m, bool cont = true, Event* eout = nullptr, bool* pending = nullptr)
+                          const Medium& m, bool cont = true)
 {
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
@@ -1448,33 +1439,9 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
         SECT_END(tr, SECT_M_TR);
     }
     SECT_BEGIN(ss);
-    bool pend = false;
-    dv3 Ld = single_scattering<COUNT, LT, DS>(S, smp, xt, p.d, e.src, sigma_t, ws, sigma_s, T, probSource, zero_ok, &pend);
+    dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, ws, sigma_s, T, probSource, zero_ok);
     SECT_END(ss, SECT_M_SS);
-    if (DS && pend) {
-        p.o = xt;
-        eout->t = T;
-        eout->pdf = e.pdf;
-        *pending = true;
-        return;
-    }
     medium_tail<EST, COUNT>(smp, p, Ld, T, e.pdf, xt, m, cont);
-}
-
-/* the rest of a point-light medium event whose shadow ray was deferred (medium_event DS): the shadow
- * ray from the light toward the scatter point p.o, its Ld, then medium_tail -- the operations and
- * draws of the undivided event */
-template <int EST, bool COUNT>
-VPT_DEV void medium_shadow_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
-                                 const Medium& m, bool cont)
-{
-    const double sigma_t = m.sigma_a + m.sigma_s;
-    constexpr bool ws = EST == 1 || EST == 4;
-    const double T = ws ? e.t : 1.0;
-    SECT_BEGIN(swi);
-    const dv3 Ld = point_shadow_ld(S, smp, p.o, p.d, e.src, sigma_t, ws, m.sigma_s, T, 1.0 / S->n_emit);
-    SECT_END(swi, SECT_M_SHADOW_IN);
-    medium_tail<EST, COUNT>(smp, p, Ld, T, e.pdf, p.o, m, cont);
 }
 
 /* iterativePathTracer, include/shadeMethods.h:104-163 (estimator 5): surface-only path tracing.

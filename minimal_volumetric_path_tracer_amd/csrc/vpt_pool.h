@@ -72,20 +72,11 @@ namespace vpt {
  * 32 48.39 / 215.9; one round only (VPT_PREP_ROUNDS=1) 48.11 / 218.1 */
 #define VPT_PREP_MORE_MIN 24
 #endif
-/* Deferred point-light shadow rays: a medium event toward a point light casts the shadow ray only when
- * its light cone misses the light (13-20 % of them); such a batch ran that ray with ~8 of 64
- * lanes (2.6 % of the kernel's wave-time, profiles/r03/sections_ff_prep.txt).  With this ring the lanes
- * stop after the cone (scatter point, transmittance and pdf kept in the task) and a later batch casts
- * 64 of those rays at once (medium_shadow_event) -- the same operations and draws. */
-#ifndef VPT_SHADOW_RING
-#define VPT_SHADOW_RING 0
-#endif
 constexpr int NF = 18;      /* doubles per task */
 /* rings: A; S diffuse x (sphere light, point light), metal, other; M (sphere light, point light);
- * with VPT_KILL_RINGS the four diffuse-surface / medium rings again for tasks the event ends; with
- * VPT_SHADOW_RING the deferred shadow rays */
-constexpr int R_A = 0, R_S = 1, R_M = 5, R_SD = 7, R_MD = 9, R_SH = VPT_KILL_RINGS ? 11 : 7;
-constexpr int NR = R_SH + (VPT_SHADOW_RING ? 1 : 0), R_DONE = NR;
+ * with VPT_KILL_RINGS the four diffuse-surface / medium rings again for tasks the event ends */
+constexpr int R_A = 0, R_S = 1, R_M = 5, R_SD = 7, R_MD = 9;
+constexpr int NR = VPT_KILL_RINGS ? 11 : 7, R_DONE = NR;
 /* the scheduler's counters (TaskPool::ctl): ring tails, ring heads, slots retired, the unit ring's
  * tail, queue exhausted, refill in progress, the unit ring's head (one lane-parallel read fetches all) */
 constexpr int C_TAIL = 0, C_HEAD = NR, C_DONE = 2 * NR, C_UTAIL = 2 * NR + 1, C_EXH = 2 * NR + 2, C_RFL = 2 * NR + 3,
@@ -136,7 +127,7 @@ struct TaskPool {
     uint32_t pix[POOL];      /* x | camera row << 16 of the unit's pixel */
     uint32_t c1[POOL];       /* one past the unit's last sample; 0 = no unit */
     uint32_t samp[POOL];     /* next sample to start | in_path << 31 */
-    uint32_t evw[POOL];      /* depth | id << 16 | src << 24 | shadow-dies << 30 | killed << 31 */
+    uint32_t evw[POOL];      /* depth | id << 16 | src << 24 | killed << 31 */
     uint16_t ring[NR][POOL]; /* slots waiting, per ring */
     /* the scheduler's counters, contiguous so that one lane-parallel LDS read fetches them all:
      * monotonic ring tails and heads, slots retired, the unit ring's tail, queue exhausted */
@@ -238,8 +229,6 @@ struct Task {
     unsigned c1;     /* one past the unit's last sample; 0 = the task needs a unit */
     unsigned i;      /* next sample to start */
     bool in_path, killed;
-    bool pend;       /* the event stopped for a deferred shadow ray (ring R_SH) */
-    bool sh_die;     /* ... and the path ends after it (the M ring was kill-predicted) */
 };
 
 /* the fields only stage A reads (unit, chunk sum, sample counter): loaded right before it */
@@ -265,8 +254,7 @@ __device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bo
     const uint32_t ev = sh.evw[s];
     t.p.depth = (int)(ev & 0xFFFFu);
     t.e.id = (int)((ev >> 16) & 0xFFu);
-    t.e.src = (int)((ev >> 24) & 0x3Fu);  /* (VPT_MAX_SPHERES <= 64) */
-    t.sh_die = ((ev >> 30) & 1u) != 0;
+    t.e.src = (int)((ev >> 24) & 0x7Fu);
     t.killed = (ev >> 31) != 0;
     t.X = sh.X[s];
     if (full) load_task_unit(sh, s, t);
@@ -280,7 +268,7 @@ __device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, b
     sh.f[F_LX][s] = t.p.L.x; sh.f[F_LY][s] = t.p.L.y; sh.f[F_LZ][s] = t.p.L.z;
     sh.X[s] = t.X;
     sh.evw[s] = (uint32_t)(t.p.depth & 0xFFFF) | ((uint32_t)t.e.id << 16) | ((uint32_t)t.e.src << 24) |
-                (t.sh_die ? 0x40000000u : 0u) | (t.killed ? 0x80000000u : 0u);
+                (t.killed ? 0x80000000u : 0u);
     if (full) {
         sh.f[F_TD][s] = t.e.t;  /* stage_a leaves the distance the next stage reads in e.t */
         sh.f[F_KEY][s] = __longlong_as_double((long long)t.key);
@@ -317,12 +305,6 @@ __device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sample
         if (st == R_S + 2) t.killed = surface_event_pt<COUNT, 1>(S, smp, t.p, t.e);
         else if (st == R_S) t.killed = surface_event_pt<COUNT, 0>(S, smp, t.p, t.e);
         else t.killed = surface_event_pt<COUNT, -1>(S, smp, t.p, t.e);
-    } else if (VPT_SHADOW_RING && st == R_SH) {
-        /* the deferred point-light shadow rays, then the rest of their medium events */
-        SECT_BEGIN(ev);
-        medium_shadow_event<EST, COUNT>(S, smp, t.p, t.e, m, !t.sh_die);
-        SECT_END(ev, SECT_M_TOTAL);
-        t.killed = t.sh_die || !continue_path(smp, t.p, m);
     } else {
         SECT_BEGIN(ev);
         /* a kill-predicted ring (R_SD.., R_MD..) runs its base ring's event without the continuation */
@@ -341,13 +323,9 @@ __device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sample
         } else if (st == R_M) {
             medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m, cont);
         } else {
-            medium_event<EST, COUNT, 1, VPT_SHADOW_RING != 0>(S, smp, t.p, t.e, m, cont, &t.e, &t.pend);
+            medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m, cont);
         }
         SECT_END(ev, st < R_M ? SECT_S_TOTAL : SECT_M_TOTAL);
-        if (VPT_SHADOW_RING && t.pend) {  /* the shadow ray and the roulette draw come in ring R_SH */
-            t.sh_die = !cont;
-            return;
-        }
         SECT_BEGIN(cp);
         t.killed = !cont || !continue_path(smp, t.p, m);  /* next iteration's roulette draw */
         SECT_END(cp, SECT_CONT);
@@ -600,19 +578,10 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         SECT_BEGIN(sc);
         /* ---- scheduling without a lock (ring_entry): reserve, publish, claim ---- */
         if (VPT_SCHED_PRIO) __builtin_amdgcn_s_setprio(VPT_SCHED_PRIO);
-        if (n > 0) {  /* return the finished tasks: one LDS atomic per ring reserves their positions */
+        if (n > 0) {  /* return the finished tasks: each lane reserves its ring position with one LDS atomic */
             const bool ret = lane < n && next < NR;
-            int rank = 0, cnt = 0;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const uint64_t msk = __ballot(ret && next == r);
-                if (ret && next == r) rank = __popcll(msk & below);
-                if (lane == r) cnt = __popcll(msk);
-            }
-            int base = 0;
-            if (lane < NR && cnt > 0)
-                base = __hip_atomic_fetch_add(&sh.ctl[C_TAIL + lane], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int pos = __shfl(base, ret ? next : 0) + rank;
+            int pos = 0;
+            if (ret) pos = __hip_atomic_fetch_add(&sh.ctl[C_TAIL + next], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  /* task states before their entries */
             if (ret) ((volatile uint16_t*)sh.ring[next])[pos % POOL] = ring_entry(slot, pos);
             const uint64_t md = __ballot(lane < n && next == R_DONE);
@@ -663,12 +632,21 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
             int best = 0;
             st = 0;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const int c = __builtin_amdgcn_readlane(v, C_TAIL + r) - __builtin_amdgcn_readlane(v, C_HEAD + r);
-                if (c > best) {
-                    best = c;
-                    st = r;
+            /* the fullest ring, lowest index on ties: lane r < NR holds ring r's count as the key
+             * count << 4 | (15 - r); a max over the first 16 lanes (row shifts) leaves it in lane 15 */
+            static_assert(NR <= 16, "the ring argmax runs in one DPP row");
+            {
+                const int hv = lane < NR ? lds_peek(&sh.ctl[C_HEAD + lane]) : 0;
+                const int c = v - hv;
+                int key = lane < NR && c > 0 ? (c << 4) | (15 - lane) : -1;
+                key = max(key, __builtin_amdgcn_update_dpp(-1, key, 0x111, 0xF, 0xF, false));  /* row_shr:1 */
+                key = max(key, __builtin_amdgcn_update_dpp(-1, key, 0x112, 0xF, 0xF, false));  /* row_shr:2 */
+                key = max(key, __builtin_amdgcn_update_dpp(-1, key, 0x114, 0xF, 0xF, false));  /* row_shr:4 */
+                key = max(key, __builtin_amdgcn_update_dpp(-1, key, 0x118, 0xF, 0xF, false));  /* row_shr:8 */
+                key = __builtin_amdgcn_readlane(key, 15);
+                if (key >= 0) {
+                    best = key >> 4;
+                    st = 15 - (key & 15);
                 }
             }
             if (VPT_UNLIKELY(best <= 0)) {
@@ -741,15 +719,12 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             t.killed = false;
         }
         SECT_END(ld, SECT_LOAD);
-        t.pend = false;
         if (stage != 0 && active) {
             smp.X = t.X;
             run_event<EST, COUNT>(S, smp, t, m, st);
             t.X = smp.X;
         }
-        /* a task whose event waits for its deferred shadow ray skips stage A and goes to ring R_SH */
-        next = stage_a<EST>(sh, P, S, m, smp, t, active && !(VPT_SHADOW_RING && t.pend), lane, below, dbga, D);
-        if (VPT_SHADOW_RING && t.pend) next = R_SH;
+        next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
         SECT_BEGIN(stt);
         if (active) store_task(sh, slot, t, true);
         SECT_END(stt, SECT_STORE);
