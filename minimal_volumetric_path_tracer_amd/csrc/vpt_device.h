@@ -1226,10 +1226,8 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
         /* MIS: psurf = exp(-σt t) (:1419); explicit: TrActual = Tr(x, xs), 0 on a miss (:1033-1041) */
         const double psurf = EST == 1 ? lm_exp(sigma_t * t * -1.0)
                                       : (hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0);
-        {
-            const double x = smp.next();  /* equiAngularParams2's draw (volumetricBasicFunctions.h:219) */
-            e.pdf = hit ? x : -x;          /* medium_event: eqa_medium */
-        }
+        (void)smp.next();  /* equiAngularParams2's draw (volumetricBasicFunctions.h:219), read back by eqa_medium */
+        e.pdf = psurf;     /* medium_event: eqa_medium */
         surf = EST == 1 ? smp.next() < psurf : smp.next() <= psurf;  /* :1423 / :1096 */
     }
     if (!surf) return EV_MED;
@@ -1349,17 +1347,17 @@ VPT_DEV bool surface_event_pt(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     return false;
 }
 
-/* the deferred equi-angular arithmetic of decide(): d_final and its pdf from the
- * ray, the light, tMax = e.t and the draw carried in e.pdf -- the operations decide() performed in
- * round 2, in the same order */
+/* the deferred equi-angular arithmetic of decide(): d_final and its pdf from the ray, the light,
+ * tMax = e.t, decide()'s psurf (carried in e.pdf) and its equi-angular draw -- the value of the
+ * stream state one draw before X, the state after decide()'s last draw (the surface coin): erand48
+ * steps back by X -> a^-1 (X - c) mod 2^48 -- the operations decide() performed in round 2, in the
+ * same order */
 template <int EST>
-VPT_DEV void eqa_medium(const DevScene* __restrict__ S, const Path& p, const Event& e, double sigma_t, double& dist,
+VPT_DEV void eqa_medium(const DevScene* __restrict__ S, const Path& p, const Event& e, uint64_t X, double& dist,
                         double& pdf)
 {
-    const double t = e.t, x = vm_fabs(e.pdf);
-    const bool hit = !__builtin_signbit(e.pdf);
-    const double psurf = EST == 1 ? lm_exp(sigma_t * t * -1.0)
-                                  : (hit ? transmitance(p.o, add(p.o, scl(p.d, t)), sigma_t) : 0.0);
+    const double t = e.t, psurf = e.pdf;
+    const double x = vpt_erand48_value(((X - 0xBull) * 0xDFE05BCB1365ull) & 0xFFFFFFFFFFFFull);
     double D = 0, ta = 0, tb = 0, sd = 0;
     dist = equiangular_setup(S, e.src, t, p.o, p.d, x, D, ta, tb, sd);
     pdf = equiangular_prob(D, ta, tb, sd) * (1 - psurf);
@@ -1413,7 +1411,7 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
     const double continueprob = 0.6;
     Event e = e0;
     SECT_BEGIN(eq);
-    if (EST == 1 || EST == 4) eqa_medium<EST>(S, p, e0, sigma_t, e.dist, e.pdf);
+    if (EST == 1 || EST == 4) eqa_medium<EST>(S, p, e0, smp.X, e.dist, e.pdf);
     SECT_END(eq, SECT_M_EQA);
     dv3 xt = add(p.o, scl(p.d, e.dist));
     if (EST == 3) {  /* implicit: vptShadeMethods.h:1000-1006 */

@@ -122,12 +122,10 @@ enum { F_OX = 0, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_BX, F_BY, F_BZ, F_LX, F_LY, F_L
        F_PDF };
 
 struct TaskPool {
-    double f[NF][POOL];      /* SoA: one array per field */
+    double2 f2[NF / 2][POOL]; /* SoA of field pairs (F_OX, F_OY), (F_OZ, F_DX), ...: one 16-B LDS access per pair */
     uint64_t X[POOL];        /* erand48 state */
-    uint32_t pix[POOL];      /* x | camera row << 16 of the unit's pixel */
-    uint32_t c1[POOL];       /* one past the unit's last sample; 0 = no unit */
-    uint32_t samp[POOL];     /* next sample to start | in_path << 31 */
-    uint32_t evw[POOL];      /* depth | id << 16 | src << 24 | killed << 31 */
+    uint4 w[POOL];           /* pix (x | camera row << 16), c1 (one past the unit's last sample; 0 = no unit),
+                              * samp (next sample | in_path << 31), evw (depth | id << 16 | src << 24 | killed << 31) */
     uint16_t ring[NR][POOL]; /* slots waiting, per ring */
     /* the scheduler's counters, contiguous so that one lane-parallel LDS read fetches them all:
      * monotonic ring tails and heads, slots retired, the unit ring's tail, queue exhausted */
@@ -231,53 +229,51 @@ struct Task {
     bool in_path, killed;
 };
 
-/* the fields only stage A reads (unit, chunk sum, sample counter): loaded right before it */
-__device__ __forceinline__ void load_task_unit(const TaskPool& sh, int s, Task& t)
+/* the task state in 11 LDS accesses (9 field pairs, X, the four words) instead of 23 with one array per
+ * field: a batch's slots are scattered, so each access pays bank conflicts, and fewer, wider accesses
+ * pay them fewer times (A/B: FF 43.30 -> 42.90 ms) */
+__device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bool)
 {
-    t.acc = mk(sh.f[F_AX][s], sh.f[F_AY][s], sh.f[F_AZ][s]);
-    t.key = (uint64_t)__double_as_longlong(sh.f[F_KEY][s]);
-    t.pix = sh.pix[s];
-    t.c1 = sh.c1[s];
-    const uint32_t sm = sh.samp[s];
-    t.i = sm & 0x7FFFFFFFu;
-    t.in_path = (sm >> 31) != 0;
-}
-
-__device__ __forceinline__ void load_task(const TaskPool& sh, int s, Task& t, bool full)
-{
-    t.p.o = mk(sh.f[F_OX][s], sh.f[F_OY][s], sh.f[F_OZ][s]);
-    t.p.d = mk(sh.f[F_DX][s], sh.f[F_DY][s], sh.f[F_DZ][s]);
-    t.p.beta = mk(sh.f[F_BX][s], sh.f[F_BY][s], sh.f[F_BZ][s]);
-    t.p.L = mk(sh.f[F_LX][s], sh.f[F_LY][s], sh.f[F_LZ][s]);
-    t.e.t = t.e.dist = sh.f[F_TD][s];
-    t.e.pdf = sh.f[F_PDF][s];
-    const uint32_t ev = sh.evw[s];
+    static_assert(F_OX == 0 && F_DX == 3 && F_BX == 6 && F_LX == 9 && F_AX == 12 && F_TD == 15 && F_KEY == 16 &&
+                      F_PDF == 17, "the field pairs below");
+    const double2 a = sh.f2[0][s], b = sh.f2[1][s], c = sh.f2[2][s], d = sh.f2[3][s], e = sh.f2[4][s];
+    const double2 f = sh.f2[5][s], g = sh.f2[6][s], h = sh.f2[7][s], k = sh.f2[8][s];
+    t.p.o = mk(a.x, a.y, b.x);
+    t.p.d = mk(b.y, c.x, c.y);
+    t.p.beta = mk(d.x, d.y, e.x);
+    t.p.L = mk(e.y, f.x, f.y);
+    t.acc = mk(g.x, g.y, h.x);
+    t.e.t = t.e.dist = h.y;
+    t.key = (uint64_t)__double_as_longlong(k.x);
+    t.e.pdf = k.y;
+    t.X = sh.X[s];
+    const uint4 w = sh.w[s];
+    t.pix = w.x;
+    t.c1 = w.y;
+    t.i = w.z & 0x7FFFFFFFu;
+    t.in_path = (w.z >> 31) != 0;
+    const uint32_t ev = w.w;
     t.p.depth = (int)(ev & 0xFFFFu);
     t.e.id = (int)((ev >> 16) & 0xFFu);
     t.e.src = (int)((ev >> 24) & 0x7Fu);
     t.killed = (ev >> 31) != 0;
-    t.X = sh.X[s];
-    if (full) load_task_unit(sh, s, t);
 }
 
-__device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, bool full)
+__device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, bool)
 {
-    sh.f[F_OX][s] = t.p.o.x; sh.f[F_OY][s] = t.p.o.y; sh.f[F_OZ][s] = t.p.o.z;
-    sh.f[F_DX][s] = t.p.d.x; sh.f[F_DY][s] = t.p.d.y; sh.f[F_DZ][s] = t.p.d.z;
-    sh.f[F_BX][s] = t.p.beta.x; sh.f[F_BY][s] = t.p.beta.y; sh.f[F_BZ][s] = t.p.beta.z;
-    sh.f[F_LX][s] = t.p.L.x; sh.f[F_LY][s] = t.p.L.y; sh.f[F_LZ][s] = t.p.L.z;
+    sh.f2[0][s] = double2{t.p.o.x, t.p.o.y};
+    sh.f2[1][s] = double2{t.p.o.z, t.p.d.x};
+    sh.f2[2][s] = double2{t.p.d.y, t.p.d.z};
+    sh.f2[3][s] = double2{t.p.beta.x, t.p.beta.y};
+    sh.f2[4][s] = double2{t.p.beta.z, t.p.L.x};
+    sh.f2[5][s] = double2{t.p.L.y, t.p.L.z};
+    sh.f2[6][s] = double2{t.acc.x, t.acc.y};
+    sh.f2[7][s] = double2{t.acc.z, t.e.t};  /* stage_a leaves the distance the next stage reads in e.t */
+    sh.f2[8][s] = double2{__longlong_as_double((long long)t.key), t.e.pdf};
     sh.X[s] = t.X;
-    sh.evw[s] = (uint32_t)(t.p.depth & 0xFFFF) | ((uint32_t)t.e.id << 16) | ((uint32_t)t.e.src << 24) |
-                (t.killed ? 0x80000000u : 0u);
-    if (full) {
-        sh.f[F_TD][s] = t.e.t;  /* stage_a leaves the distance the next stage reads in e.t */
-        sh.f[F_KEY][s] = __longlong_as_double((long long)t.key);
-        sh.f[F_PDF][s] = t.e.pdf;
-        sh.f[F_AX][s] = t.acc.x; sh.f[F_AY][s] = t.acc.y; sh.f[F_AZ][s] = t.acc.z;
-        sh.pix[s] = t.pix;
-        sh.c1[s] = t.c1;
-        sh.samp[s] = t.i | (t.in_path ? 0x80000000u : 0u);
-    }
+    sh.w[s] = uint4{t.pix, t.c1, t.i | (t.in_path ? 0x80000000u : 0u),
+                    (uint32_t)(t.p.depth & 0xFFFF) | ((uint32_t)t.e.id << 16) | ((uint32_t)t.e.src << 24) |
+                        (t.killed ? 0x80000000u : 0u)};
 }
 
 /* the finished unit's chunk sum -> partials[chunk][shard row][x] */
@@ -524,7 +520,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         } else {
             result = R_M + (EST == 3 ? 0 : sph_flag(S->m_point, t.e.src));
             /* one slot (F_TD): stage M reads the sampled distance -- or, for the deferred
-             * equi-angular estimators, tMax (with the draw in F_PDF) */
+             * equi-angular estimators, tMax (with decide()'s psurf in F_PDF) */
             if (!(EST == 1 || EST == 4)) t.e.t = t.e.dist;
             /* a medium event: the light cone's two draws and the phase sample's two, then the roulette */
             if constexpr (kill_predicted_est<EST>() && !COUNT) {
@@ -551,9 +547,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
     const int tid = threadIdx.x, lane = tid & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     for (int j = tid; j < POOL; j += VPT_POOL_THREADS) {
-        sh.c1[j] = 0;
-        sh.samp[j] = 0;
-        sh.evw[j] = 0;
+        sh.w[j] = uint4{0u, 0u, 0u, 0u};
         sh.ring[R_A][j] = (uint16_t)j;  /* = ring_entry(j, j): lap 0 */
         for (int r = 1; r < NR; ++r) sh.ring[r][j] = (uint16_t)(LAP_MASK << SLOT_BITS);  /* no lap-0 entry yet */
     }
