@@ -128,12 +128,21 @@ def main():
                          capture_output=True, text=True).stdout
     blocks = [b for b in sym.split("\n\n")]
     table = collections.defaultdict(collections.Counter)
+    rare = 0
     for (a, op, f), blk in zip(insts, blocks):
         frames = [l for i, l in enumerate(blk.strip().splitlines()) if i % 2 == 0]
+        # the rare rings' code (metal / other materials: surface_event<.., MK = 1 or -1>; the sequential
+        # MISv2, which the diffuse rings compile but do not run with two MIS lights) is left out: the
+        # budget is of what the hot rings execute
+        if any(re.search(r"surface_event<\d+, false, (1|-1),", g) for g in frames) or \
+                any(g.startswith("mis_v2<") for g in frames):
+            rare += 1
+            continue
         sec = section(frames) if f == kname else "call " + re.sub(r"^_ZL?\d+", "", f)[:28]
         table[sec][op_class(op)] += 1
     hdr = f"{'section':22s} {'total':>6s} " + " ".join(f"{c:>8s}" for c in CLASSES) + "  non-fp64 VALU"
     print(f"# static opcode classes of {kname} ({co}); 'x entries' = static x section entries per launch")
+    print(f"# ({rare} instructions of the rare rings -- metal / other materials, sequential MISv2 -- left out)")
     print(hdr)
     tot = collections.Counter()
     for sec in sorted(table, key=lambda s: -sum(table[s].values())):

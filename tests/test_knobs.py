@@ -1,0 +1,32 @@
+"""Every compile-time arm the release build does not take still compiles: the
+kept structural knob (VPT_KILL_RINGS=0, the pool without kill-predicting rings) and the debug builds
+(section timers, scheduler statistics and timelines, the round-1 wave kernel behind VPT_DEBUG_ENV).
+A device-side syntax and template-instantiation check of csrc/vpt_kernels.hip for gfx950 -- seconds,
+no GPU; the A/B builds themselves go through scripts/build_variant.sh."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+HIPCC = "/opt/rocm/bin/hipcc"
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "minimal_volumetric_path_tracer_amd",
+                    "csrc")
+
+ARMS = {
+    "no_kill_rings": ["-DVPT_KILL_RINGS=0"],
+    "sections": ["-DVPT_SECTIONS=1"],
+    "sections_no_kill_rings": ["-DVPT_SECTIONS=1", "-DVPT_KILL_RINGS=0"],
+    "pool_stats": ["-DVPT_POOL_DEBUG=1"],
+    "pool_timeline": ["-DVPT_POOL_DEBUG=2"],
+    "debug_env": ["-DVPT_DEBUG_ENV=1"],
+}
+
+
+@pytest.mark.skipif(not (os.path.exists(HIPCC) or shutil.which("hipcc")), reason="hipcc not installed")
+@pytest.mark.parametrize("arm", sorted(ARMS))
+def test_knob_arm_compiles(arm):
+    cmd = [HIPCC, "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=off", "-fsyntax-only", "--cuda-device-only",
+           "-Wno-unused-command-line-argument"] + ARMS[arm] + ["vpt_kernels.hip"]
+    r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
