@@ -59,7 +59,7 @@ namespace vpt {
 #define VPT_SCHED_PRIO 3    /* s_setprio level of the scheduler's critical section (0: off; A/B 3 vs 0: +0.7 %) */
 #endif
 #ifndef VPT_PREP_TRIES
-#define VPT_PREP_TRIES 2    /* samples a lane may start per preparation round (A/B 1 / 2 / 4 / 8: FF 52.16 / 52.02 / 53.70 / 53.85 ms, MIS 248.1 / 245.2 / 251.9 / 252.0) */
+#define VPT_PREP_TRIES 3    /* samples a lane may start per preparation round (round 2, A/B 1 / 2 / 4 / 8: FF 52.16 / 52.02 / 53.70 / 53.85 ms, MIS 248.1 / 245.2 / 251.9 / 252.0; round 4, with the kill rings every lane of a dying batch restarts: 2 / 3: FF 42.84 / 42.75, MIS + HG 194.1 / 193.5) */
 #endif
 #ifndef VPT_PREP_ROUNDS
 #define VPT_PREP_ROUNDS 2   /* stage-A preparation rounds per batch before unready lanes park (0: no cap; round-2 A/B 1 / 2 / 3 / none: 4949 / 5104 / 5052 / 5020 Ms/s; round 3: see VPT_PREP_MORE_MIN) */
@@ -583,9 +583,12 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                 __hip_atomic_fetch_add(&sh.ctl[C_DONE], __popcll(md), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         /* keep the unit ring stocked (the queue atomic's latency is paid once per 128 units); one
-         * wave at a time, claimed by a flag */
+         * wave at a time, claimed by a flag.  The counters read here serve the first claim attempt
+         * below as well (re-read after a refill and on every retry). */
+        int vc = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+        int hc = lane < NR ? lds_peek(&sh.ctl[C_HEAD + lane]) : 0;
         {
-            const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+            const int v = vc;
             if (dbg && !seen_exh && __builtin_amdgcn_readlane(v, C_EXH)) {
                 seen_exh = true;
                 if (lane == 0) dbg_tl(stats, 1, false);
@@ -616,21 +619,23 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                     }
                     if (lane == 0) __hip_atomic_store(&sh.ctl[C_RFL], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+                vc = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+                hc = lane < NR ? lds_peek(&sh.ctl[C_HEAD + lane]) : 0;
             }
         }
         /* take a batch of the fullest ring: read its published entries, then claim them by one CAS
          * on the ring's head (a claim never covers an entry that is not yet written) */
         int st = 0, take = 0;
         bool fin = false;
-        while (true) {
-            const int v = lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
+        for (bool first = true;; first = false) {
+            const int v = first ? vc : lane < NCTL ? lds_peek(&sh.ctl[lane]) : 0;
             int best = 0;
             st = 0;
             /* the fullest ring, lowest index on ties: lane r < NR holds ring r's count as the key
              * count << 4 | (15 - r); a max over the first 16 lanes (row shifts) leaves it in lane 15 */
             static_assert(NR <= 16, "the ring argmax runs in one DPP row");
             {
-                const int hv = lane < NR ? lds_peek(&sh.ctl[C_HEAD + lane]) : 0;
+                const int hv = first ? hc : lane < NR ? lds_peek(&sh.ctl[C_HEAD + lane]) : 0;
                 const int c = v - hv;
                 int key = lane < NR && c > 0 ? (c << 4) | (15 - lane) : -1;
                 key = max(key, __builtin_amdgcn_update_dpp(-1, key, 0x111, 0xF, 0xF, false));  /* row_shr:1 */
