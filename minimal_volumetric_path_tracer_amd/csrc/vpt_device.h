@@ -871,7 +871,37 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     int ids[3] = {0, 0, 0};
     bool hits[3];
     SECT_BEGIN(mi);
-    scene_intersect_n<3>(S, smp, x, dirs, tt, ids, hits);
+    /* The BSDF-sampled ray (dirs[2]) is read only through the radiance of what it hits (rayTracer):
+     * when its det (b^2 - |oc|^2 + r^2, the operations Sphere::intersect performs) is negative for every
+     * sphere with a nonzero radiance, in every lane, no such sphere can be its nearest contact, the
+     * radiance is (0, 0, 0) whatever it hits, and only the two light rays are intersected -- the same
+     * values (A/B: FF 42.82 -> 42.27 ms, MIS + HG 193.6 -> 191.2 ms; testing contact itself, root and
+     * tact > 0.0001, skips more batches but costs more: 42.31 / 191.8 ms) */
+    bool skip2 = false;
+    if (S->emit_all_radiance) {
+        bool maybe = false;
+        for (int j = 0; j < S->n_emit; ++j) {
+            const GeoSphere g = S->geo[S->emit[j]];
+            const double ocx = x.x - g.px, ocy = x.y - g.py, ocz = x.z - g.pz;
+            const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
+            const double b = ocx * dirs[2].x + ocy * dirs[2].y + ocz * dirs[2].z;
+            maybe = maybe || !(b * b - cc + g.r2 < 0);
+        }
+        skip2 = __ballot(maybe) == 0;
+    }
+    if (skip2) {
+        const dv3 d2[2] = {dirs[0], dirs[1]};
+        double t2[2];
+        int i2[2] = {0, 0};
+        bool h2[2];
+        scene_intersect_n<2>(S, smp, x, d2, t2, i2, h2);
+        smp.tests(S->n);  /* (counting mode: the skipped ray's tests) */
+        tt[0] = t2[0], tt[1] = t2[1], tt[2] = 0.0;
+        ids[0] = i2[0], ids[1] = i2[1];
+        hits[0] = h2[0], hits[1] = h2[1], hits[2] = false;
+    } else {
+        scene_intersect_n<3>(S, smp, x, dirs, tt, ids, hits);
+    }
     SECT_END(mi, SECT_S_MIS_ISECT);
     /* ---- the reference's arithmetic */
     dv3 mc = mk(0, 0, 0);

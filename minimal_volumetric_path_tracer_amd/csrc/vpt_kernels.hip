@@ -835,6 +835,10 @@ int vpt_set_scene(vpt_context* ctx, const vpt_sphere* s, int n)
     }
     h.n_non3 = n - h.n_mat3;
     vpt_erand48_jump(2 * h.n_mis + 5, &h.kp_sa, &h.kp_sc);
+    h.emit_all_radiance = 1;
+    for (int i = 0; i < n; ++i)
+        if (!h.geo[i].emitter && (s[i].radiance[0] != 0 || s[i].radiance[1] != 0 || s[i].radiance[2] != 0))
+            h.emit_all_radiance = 0;
     HIP_OK(hipSetDevice(ctx->device));
     HIP_OK(hipMemcpy(ctx->d_scene, &h, sizeof h, hipMemcpyHostToDevice));
     ctx->h_scene = h;

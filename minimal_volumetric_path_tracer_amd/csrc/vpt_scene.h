@@ -29,7 +29,8 @@ struct DevScene {
     int32_t n_mis;      /* spheres with r > 0 && radiance.x > 0 (MISv2 light loop) */
     int32_t n_mat3;     /* material-3 spheres */
     int32_t n_non3;     /* n - n_mat3 */
-    int32_t pad_[3];
+    int32_t emit_all_radiance; /* 1: every sphere with a nonzero radiance channel is in emit[] (MISv2's BSDF-ray skip) */
+    int32_t pad_[2];
     /* per-sphere flags as bit masks (bit i = sphere i; VPT_MAX_SPHERES <= 64), read with a per-lane id
      * by shifts of wave-uniform words instead of per-lane loads of GeoSphere fields */
     uint64_t m_emitter, m_point, m_mat3, m_skey1, m_skey2;  /* skey = m_skey1 bit + 2 * m_skey2 bit */
