@@ -578,7 +578,7 @@ def main():
         for f, body in fns:
             args_ = "double a0" + (", double a1" if f.nargs == 2 else "")
             init = "    x0 = gl_u(a0);" + (" x1 = gl_u(a1);" if f.nargs == 2 else "") + "\n"
-            w("GL_FN double gl_%s(%s)\n{\n" % (f.name, args_))
+            w("GL_ENTRY double gl_%s(%s)\n{\n" % (f.name, args_))
             w(prologue(f, init, body))
             w("\n".join(body).replace("return x0;", "return gl_f(x0);").replace(
                 "return gl_h_", "return gl_f(gl_h_").replace("(r_di, x0, x1);", "(r_di, x0, x1));").replace(

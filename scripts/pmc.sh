@@ -23,7 +23,7 @@ i=0
 for p in "${PASSES[@]}"; do
     i=$((i + 1))
     echo "== pass $i: $p"
-    timeout -k 10 600 rocprofv3 --pmc $p --kernel-trace -d "$OUT/p$i" -o run --output-format csv -- \
+    timeout -k 10 ${PMC_TIMEOUT:-600} rocprofv3 --pmc $p --kernel-trace -d "$OUT/p$i" -o run --output-format csv -- \
         python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
     rc=$?
     echo "rc=$rc"
