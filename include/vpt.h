@@ -33,7 +33,8 @@ typedef enum {
     VPT_E_NO_EMITTER = -3,     /* reserved */
     VPT_E_UNSUPPORTED = -4,    /* material id outside {0,1,2,3} */
     VPT_E_HIP = -5,            /* HIP runtime error (message in vpt_last_error) */
-    VPT_E_IO = -6              /* file could not be written */
+    VPT_E_IO = -6,             /* file could not be written */
+    VPT_E_INTERNAL = -7        /* an internal invariant failed (message in vpt_last_error) */
 } vpt_status;
 
 #define VPT_MAX_SPHERES 64

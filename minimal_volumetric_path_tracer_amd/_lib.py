@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("VPT_LIB") or os.path.join(PKG_DIR, "libvpt.so")
 CLI_PATH = os.path.join(PKG_DIR, "vpt")
 
 VPT_OK = 0
-VPT_E_INVALID, VPT_E_TOO_MANY, VPT_E_NO_EMITTER, VPT_E_UNSUPPORTED, VPT_E_HIP, VPT_E_IO = -1, -2, -3, -4, -5, -6
+VPT_E_INVALID, VPT_E_TOO_MANY, VPT_E_NO_EMITTER, VPT_E_UNSUPPORTED, VPT_E_HIP, VPT_E_IO, VPT_E_INTERNAL = \
+    -1, -2, -3, -4, -5, -6, -7
 VPT_MAX_SPHERES = 64
 FREE_FLIGHT, MIS_EQUIANGULAR, EXPLICIT_FREE, IMPLICIT_FREE, EXPLICIT_EQUIANGULAR, SURFACE_PT, RAY_MARCHING = 0, 1, 2, 3, 4, 5, 6  # vpt_estimator
 RAY_MARCHING_SA, RAY_MARCHING_GLOBAL, RAY_MARCHING_EXPLICIT = 7, 8, 9

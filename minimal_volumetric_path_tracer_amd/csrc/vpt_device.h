@@ -129,11 +129,21 @@ VPT_DEV dv3 scl(dv3 a, double s) { return dv3{a.x * s, a.y * s, a.z * s}; }
 VPT_DEV dv3 mul(dv3 a, dv3 b) { return dv3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 VPT_DEV double dot(dv3 a, dv3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 VPT_DEV dv3 cross(dv3 a, dv3 b) { return dv3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
-VPT_DEV dv3 nrm(dv3 a) { return scl(a, vm_inv_sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); }  /* 1.0 / sqrt(|a|^2) */
+#ifndef VPT_NRM_CALL
+#define VPT_NRM_CALL 0
+#endif
+VPT_DEV dv3 nrm_inl(dv3 a) { return scl(a, vm_inv_sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); }  /* 1.0 / sqrt(|a|^2) */
+#if VPT_NRM_CALL
+/* the reference's normalize out of line: ~100 sites in the pool kernel, ~30 instructions each */
+__device__ static __attribute__((noinline)) dv3 nrm(dv3 a) { return nrm_inl(a); }
+#else
+VPT_DEV dv3 nrm(dv3 a) { return nrm_inl(a); }
+#endif
 
 struct Counters {
     uint64_t tests;
     uint64_t iterations;
+    uint64_t draw_mismatch;  /* events whose draw count is not the pool's kill-prediction jump (trace_sample) */
 };
 
 /* Per-sample random stream + work counters.  HG g rides along (phase extension). */
@@ -787,7 +797,27 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
         contact[k] = 0;
     }
     const int n = S->n;
-    for (int i = 0; i < n; ++i) {
+    int i = 0;
+#ifndef VPT_ISECT_N_GROUP
+#define VPT_ISECT_N_GROUP 5
+#endif
+    /* VPT_ISECT_N_GROUP spheres per loop iteration: their records come in one batch of scalar loads
+     * (one wait instead of one per sphere) */
+    for (; i + VPT_ISECT_N_GROUP <= n; i += VPT_ISECT_N_GROUP) {
+#pragma unroll
+        for (int j = 0; j < VPT_ISECT_N_GROUP; ++j) {
+            const GeoSphere g = S->geo[i + j];
+            const double ocx = o.x - g.px, ocy = o.y - g.py, ocz = o.z - g.pz;
+            const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const double b = ocx * d[k].x + ocy * d[k].y + ocz * d[k].z;
+                const double det = b * b - cc + g.r2;
+                sphere_take(sphere_tact(b, det), i + j, tmin[k], id[k], contact[k]);
+            }
+        }
+    }
+    for (; i < n; ++i) {
         const GeoSphere g = S->geo[i];
         const double ocx = o.x - g.px, ocy = o.y - g.py, ocz = o.z - g.pz;
         const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
@@ -806,16 +836,33 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
     }
 }
 
+/* The next iteration's nearest hit, found inside an event's own intersection pass: the continuation
+ * ray leaves the event's vertex, like the event's own rays, so it rides in their pass over the
+ * spheres (oc and |oc|^2 formed once) and decide() takes it instead of casting the ray again.  The
+ * same operations per sphere as scene_intersect_grouped, in index order: t = tmin (0 on a miss),
+ * id unchanged (0) on a miss. */
+struct ContHit {
+    double t;
+    int id;
+    bool hit;
+};
+
 /* MISv2 (include/misSamplingFunctions.h:96-170) for a scene with exactly two MIS lights, same bits
  * and draws as mis_v2: every draw of MISv2 precedes, and none depends on, the three ray casts
  * (the two light samples of muestreoSA, :163-206, and the BSDF sample of uniform / softDielectric
  * / microfacet), so the draws and directions are taken first in the reference's order, the three
  * rays from x are intersected in one pass (scene_intersect_n), and the arithmetic is then done in
- * the reference's order. */
+ * the reference's order.
+ * CONT (diffuse surfaces, MK == 0, of a path that continues): bdsf's cosine sample -- the next two
+ * draws of the stream after MISv2's, and no draw or ray of MISv2 depends on it -- is taken here too
+ * (*wcont: the raw sample bdsf returns in aux), and its ray nrm(*wcont) from x joins the pass (*ch). */
 template <bool COUNT, int MK = -1>
 VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray,
-                              double alpha, double sigma_t)
+                              double alpha, double sigma_t, dv3* wcont = nullptr, ContHit* ch = nullptr)
 {
+    /* ch != nullptr (wave-uniform): the continuation joins the pass -- diffuse surfaces only (the
+     * caller's ring fixes MK = 0); counting mode never passes it (decide() counts the ray) */
+    const bool cont = MK == 0 && !COUNT && ch != nullptr;
     const int omat = mat_of<MK>(S, obj);
     const dv3 wo = scl(wray, -1);
     /* ---- draws and directions, in the reference's order */
@@ -866,6 +913,11 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         wi_m = nrm(add(scl(wo_l, -1), scl(scl(wh_m, 2), dot(wh_m, wo_l))));
         dirs[2] = nrm(from_local(n, wi_m.x, wi_m.y, wi_m.z));
     }
+    dv3 dcont = mk(0, 0, 0);
+    if (cont) {  /* bdsf (vptShadeMethods.h:16-59, diffuse): cosineHemispheric, then nrm in the caller */
+        *wcont = cosine_hemispheric(smp, n);
+        dcont = nrm(*wcont);
+    }
     /* ---- the three ray casts from x */
     double tt[3];
     int ids[3] = {0, 0, 0};
@@ -889,7 +941,30 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         }
         skip2 = __ballot(maybe) == 0;
     }
-    if (skip2) {
+    if (cont) {
+        if (skip2) {
+            const dv3 d3[3] = {dirs[0], dirs[1], dcont};
+            double t3[3];
+            int i3[3] = {0, 0, 0};
+            bool h3[3];
+            scene_intersect_n<3>(S, smp, x, d3, t3, i3, h3);
+            smp.tests(S->n);  /* (counting mode: the skipped ray's tests) */
+            tt[0] = t3[0], tt[1] = t3[1], tt[2] = 0.0;
+            ids[0] = i3[0], ids[1] = i3[1];
+            hits[0] = h3[0], hits[1] = h3[1], hits[2] = false;
+            *ch = ContHit{t3[2], i3[2], h3[2]};
+        } else {
+            const dv3 d4[4] = {dirs[0], dirs[1], dirs[2], dcont};
+            double t4[4];
+            int i4[4] = {0, 0, 0, 0};
+            bool h4[4];
+            scene_intersect_n<4>(S, smp, x, d4, t4, i4, h4);
+            tt[0] = t4[0], tt[1] = t4[1], tt[2] = t4[2];
+            ids[0] = i4[0], ids[1] = i4[1], ids[2] = i4[2];
+            hits[0] = h4[0], hits[1] = h4[1], hits[2] = h4[2];
+            *ch = ContHit{t4[3], i4[3], h4[3]};
+        }
+    } else if (skip2) {
         const dv3 d2[2] = {dirs[0], dirs[1]};
         double t2[2];
         int i2[2] = {0, 0};
@@ -1075,11 +1150,15 @@ VPT_DEV dv3 point_shadow_ld(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
     return Ld;
 }
 
+/* CONT (a path that continues): the phase sample of the continuation -- the stream's next two draws
+ * after the light cone's, read by nothing here -- is taken right after the cone (*wcont) and its ray
+ * from xt joins the cone ray's pass over the spheres (*ch, ContHit) */
 template <bool COUNT, int LT = -1>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
 VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
                               double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource,
-                              bool zero_ok = false)
+                              bool zero_ok = false, dv3* wcont = nullptr, ContHit* ch = nullptr)
 {
+    const bool cont = !COUNT && ch != nullptr;  /* wave-uniform; counting mode never passes ch */
     const double lr = LT == 1 ? 0.0 : S->sph[src].r;
     const dv3 lp = sph_p(S, src);
     const dv3 rad = sph_rad(S, src);
@@ -1094,11 +1173,23 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     double cmax = LT == 1 ? (mag > 0 ? 1.0 : __builtin_nan("")) : vm_sqrt(1 - lr / mag * (lr / mag));
     dv3 wl = solid_angle_dir(smp, wc, cmax);
     double prob_wl = solid_angle_prob(cmax);
+    if (cont) *wcont = phase_sample(smp, din);
     SECT_END(sd, SECT_M_SS_DIR);
     SECT_BEGIN(si);
     double tdist;
     int idHit = 0;
-    scene_isect(S, smp, xt, wl, tdist, idHit, false);
+    if (cont) {
+        const dv3 d2[2] = {wl, *wcont};
+        double t2[2];
+        int i2[2] = {0, 0};
+        bool h2[2];
+        scene_intersect_n<2>(S, smp, xt, d2, t2, i2, h2);
+        tdist = t2[0];
+        idHit = i2[0];
+        *ch = ContHit{t2[1], i2[1], h2[1]};
+    } else {
+        scene_isect(S, smp, xt, wl, tdist, idHit, false);
+    }
     SECT_END(si, SECT_M_SS_ISECT);
     SECT_BEGIN(sw);
     if (src == idHit) {
@@ -1106,7 +1197,7 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         /* a point light's cone (cmax == 1: prob_wl = +inf) scores Ls * (1 / inf) = +-0 with Ls finite
          * (SURVEY H5); zero_ok: the caller's update absorbs a signed zero (finite throughput and
          * pdf), so +0 is the same result without the exponential and the phase value */
-        if (!(LT == 1 && zero_ok && cmax == 1.0)) {
+        if (!(point && zero_ok && cmax == 1.0)) {
             double it = lm_exp(sigma_t * tdist * -1.0);
             double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, wl);
             dv3 Ls = scl(scl(rad, it), ph);
@@ -1210,13 +1301,22 @@ VPT_DEV constexpr bool est_free_flight() { return EST == 0 || EST == 2 || EST ==
 /* vptShadeMethods.h:1284-1307 (FF), :1357-1426 (MIS), :1166-1205 (explicit free), :950-977
  * (implicit free), :1031-1096 (explicit): what happens to the path this iteration. */
 template <int EST, bool COUNT>
-VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, Event& e, const Medium& m)
+VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, Event& e, const Medium& m,
+                   bool have_pre = false, const ContHit& pre = ContHit{0.0, 0, false})
 {
     const double sigma_t = m.sigma_a + m.sigma_s;
     int id = 0;
-    double t;
+    double t = 0.0;
+    bool hit = false;
     SECT_BEGIN(di);
-    const bool hit = scene_intersect_grouped<VPT_DECIDE_GROUP>(S, smp, p.o, p.d, t, id);
+    /* have_pre: the ray's nearest hit came with the event that made it (ContHit); the spheres are
+     * visited only when some lane of the wave lacks one */
+    if (__ballot(!have_pre) != 0) hit = scene_intersect_grouped<VPT_DECIDE_GROUP>(S, smp, p.o, p.d, t, id);
+    if (have_pre) {
+        hit = pre.hit;
+        t = pre.t;
+        id = pre.id;
+    }
     SECT_END(di, SECT_A_ISECT);
     if constexpr (EST == 5) {  /* iterativePathTracer (shadeMethods.h:115-125): nearest hit or end */
         if (COUNT) smp.cnt.iterations++;
@@ -1270,11 +1370,17 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
 
 /* surface event: point-light NEE (pLight), sphere-light MIS (MISv2), BSDF continuation (bdsf).
  * cont = false: the path ends at the next roulette draw (the pool's kill prediction), so only the
- * radiance is updated -- the continuation's draws, direction and throughput are never read. */
+ * radiance is updated -- the continuation's draws, direction and throughput are never read.
+ * CONT (diffuse, two MIS lights, a path that continues): bdsf's sample is taken inside MISv2 and the
+ * continuation ray's nearest hit comes back in *ch (ContHit) -- the same draws in the same order. */
 template <int EST, bool COUNT, int MK = -1, int PT = -1>  /* MK: material, PT: point light (1), if known */
 VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
-                           const Medium& m, bool cont = true)
+                           const Medium& m, bool cont = true, ContHit* ch = nullptr, int lk = -1)
 {
+    /* the light kind: PT when the instantiation fixes it, else lk (wave-uniform: the pool's ring) */
+    const int ptk = PT >= 0 ? PT : lk;
+    /* fused (wave-uniform): a continuing diffuse path in a scene with two MIS lights (ch from the pool) */
+    const bool fused = cont && ch != nullptr && MK == 0 && EST != 3 && !COUNT && S->n_mis == 2;
     const double sigma_t = m.sigma_a + m.sigma_s;
     const double continueprob = 0.6;
     const int id = e.id, src = e.src;
@@ -1303,7 +1409,7 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
      * Ldp + Ld == Ld: when that holds in every lane of the wave, the frames, the normalisations and
      * the transmittance of pLight are skipped -- same bits, no draws involved. */
     bool plight_zero = false;
-    if (PT == 0 && S->n_mat3 == 0) {
+    if (ptk == 0 && S->n_mat3 == 0) {
         const dv3 lx = sub(sph_p(S, src), xs);
         const double dd = dot(lx, lx);
         const double distance = vm_sqrt(dd);  /* visibility()'s test, pathTracingUtilities.h:44-51 */
@@ -1320,14 +1426,25 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     SECT_BEGIN(mis);
     /* the fused three-ray MISv2 for diffuse surfaces only: metal and dielectric take the sequential
      * one (round 3: scratch 448 -> 240 B/lane, FF 51.99 -> 51.53 ms) */
-    dv3 Ld = MK == 0 && S->n_mis == 2 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
-                                      : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
+    dv3 wcont = mk(0, 0, 0);
+    const dv3 Ld = MK == 0 && S->n_mis == 2
+             ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t, &wcont, fused ? ch : nullptr)
+             : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
     SECT_END(mis, SECT_S_MIS);
     SECT_BEGIN(bd);
     /* (the radiance update reads the throughput before bdsf's update, as in the reference) */
     if (EST == 0) p.L = add(p.L, scl(mul(add(Ldp, Ld), p.beta), (1 / continueprob)));
     else p.L = add(p.L, mul(p.beta, scl(add(Ldp, Ld), (1 / continueprob))));
-    if (cont) {
+    if (fused) {  /* bdsf for a diffuse surface (vptShadeMethods.h:16-59), its sample drawn in MISv2 */
+        const dv3 fs = scl(sph_c(S, id), (1 / VPT_PI));
+        const double pdf = hemi_cosine_prob(dot(nx, wcont));
+        const dv3 wi = nrm(wcont);
+        double cosine = dot(nx, wi);
+        p.beta = scl(scl(scl(mul(p.beta, fs), (1 / continueprob)), cosine), (1 / pdf));
+        p.o = xs;
+        p.d = wi;
+        p.depth++;
+    } else if (cont) {
         dv3 wi = mk(0, 0, 0);
         double pdf = 0;
         dv3 fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
@@ -1397,7 +1514,8 @@ VPT_DEV void eqa_medium(const DevScene* __restrict__ S, const Path& p, const Eve
  * radiance update, then -- unless the path ends at the next roulette draw (cont = false) -- the phase
  * sample and the throughput.  T: transmittance to xt, pdf: the equi-angular pdf (estimators 1, 4). */
 template <int EST, bool COUNT>
-VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double pdf, dv3 xt, const Medium& m, bool cont)
+VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double pdf, dv3 xt, const Medium& m, bool cont,
+                         const dv3* wpre = nullptr)  /* wpre: the phase sample, already drawn (single_scattering CONT) */
 {
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
@@ -1406,21 +1524,21 @@ VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double 
         p.L = add(p.L, scl(scl(mul(Ld, p.beta), (sigma_s / sigma_t)), (1 / continueprob)));
         if (!cont) return;
         SECT_BEGIN(ph);
-        dv3 wi = phase_sample(smp, p.d);
+        dv3 wi = wpre ? *wpre : phase_sample(smp, p.d);
         SECT_END(ph, SECT_M_PHASE);
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else if (EST == 2) {  /* vptShadeMethods.h:1252-1258 */
         p.L = add(p.L, mul(p.beta, scl(scl(Ld, (sigma_s / sigma_t)), (1 / continueprob))));
         if (!cont) return;
-        dv3 wi = phase_sample(smp, p.d);
+        dv3 wi = wpre ? *wpre : phase_sample(smp, p.d);
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else {
         p.L = add(p.L, mul(p.beta, scl(scl(Ld, (1 / pdf)), (1 / continueprob))));
         if (!cont) return;
         SECT_BEGIN(ph);
-        dv3 wi = phase_sample(smp, p.d);
+        dv3 wi = wpre ? *wpre : phase_sample(smp, p.d);
         SECT_END(ph, SECT_M_PHASE);
         p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / pdf));
         p.d = wi;
@@ -1432,10 +1550,11 @@ VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double 
 /* medium event: single-scattering NEE toward the picked light, phase-function continuation.
  * LT: 1 point light, 0 not, -1 unknown (the pool kernel's medium rings are keyed by it).  cont = false:
  * radiance only (surface_event). */
-template <int EST, bool COUNT, int LT = -1>
+template <int EST, bool COUNT, int LT = -1>  /* ch: the continuation fused (single_scattering), when cont */
 VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e0,
-                          const Medium& m, bool cont = true)
+                          const Medium& m, bool cont = true, ContHit* ch = nullptr)
 {
+    const bool fused = cont && ch != nullptr && EST != 3 && !COUNT;
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
     const double continueprob = 0.6;
@@ -1467,9 +1586,11 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
         SECT_END(tr, SECT_M_TR);
     }
     SECT_BEGIN(ss);
-    dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, ws, sigma_s, T, probSource, zero_ok);
+    dv3 wcont = mk(0, 0, 0);
+    const dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, ws, sigma_s, T, probSource, zero_ok,
+                                                &wcont, fused ? ch : nullptr);
     SECT_END(ss, SECT_M_SS);
-    medium_tail<EST, COUNT>(smp, p, Ld, T, e.pdf, xt, m, cont);
+    medium_tail<EST, COUNT>(smp, p, Ld, T, e.pdf, xt, m, cont, fused ? &wcont : nullptr);
 }
 
 /* iterativePathTracer, include/shadeMethods.h:104-163 (estimator 5): surface-only path tracing.
@@ -1726,12 +1847,34 @@ __device__ static dv3 trace_sample(const DevScene* __restrict__ S, Sampler<COUNT
         p.depth = 0;
         Event e;
         e.pdf = 0;
+        /* counting mode also checks the invariant the pool's kill-predicting rings rest on (vpt_pool.h
+         * stage_a): from the state after decide(), a diffuse surface event (2 n_mis + 4 draws) or a
+         * medium event (4 draws) and the next roulette draw end at the state the LCG jump predicts */
+        constexpr bool CHECK = COUNT && (EST == 0 || EST == 1 || EST == 2 || EST == 4);
+        uint64_t xd = 0, ja = 0, jc = 0;
+        bool pend = false;
         while (continue_path(smp, p, m)) {
+            if (CHECK && pend && smp.X != vpt_erand48_skip(xd, ja, jc)) smp.cnt.draw_mismatch++;
+            pend = false;
             int ev = decide<EST>(S, smp, p, e, m);
             if (ev == EV_END) break;
+            if (CHECK) {
+                xd = smp.X;
+                if (ev == EV_MED) {
+                    vpt_erand48_jump(5, &ja, &jc);
+                    pend = true;
+                } else if ((sph_flag(S->m_skey1, e.id) | sph_flag(S->m_skey2, e.id)) == 0) {
+                    ja = S->kp_sa;
+                    jc = S->kp_sc;
+                    pend = true;
+                }
+            }
             if (ev == EV_SURF) surface_event<EST>(S, smp, p, e, m);
             else medium_event<EST>(S, smp, p, e, m);
         }
+        /* (a path the roulette ended drew it too; one the depth cap ended did not) */
+        if (CHECK && pend && !(m.max_depth > 0 && p.depth >= m.max_depth) && smp.X != vpt_erand48_skip(xd, ja, jc))
+            smp.cnt.draw_mismatch++;
         return p.L;
     }
 }

@@ -72,13 +72,14 @@ __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const Dev
     const dv3 o = mk(P.o[0], P.o[1], P.o[2]), cd = mk(P.d[0], P.d[1], P.d[2]);
     const dv3 cx = mk(P.cx[0], P.cx[1], P.cx[2]), cy = mk(P.cy[0], P.cy[1], P.cy[2]);
     dv3 acc = mk(0, 0, 0);
-    uint64_t tests = 0, iters = 0;
+    uint64_t tests = 0, iters = 0, mism = 0;
     for (int i = 0; i < P.spp; ++i) {
         Sampler<COUNT> smp;
         smp.X = vpt_stream_start(P.seed, idx, (uint64_t)i);
         smp.g = P.g;
         smp.cnt.tests = 0;
         smp.cnt.iterations = 0;
+        smp.cnt.draw_mismatch = 0;
         /* jittered camera ray, src/rt.cpp:787, x draw first */
         double jx = smp.next();
         double jy = smp.next();
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const Dev
         if (COUNT) {
             tests += smp.cnt.tests;
             iters += smp.cnt.iterations;
+            mism += smp.cnt.draw_mismatch;
         }
     }
     acc = scl(acc, (1 / (double)P.spp));
@@ -107,6 +109,7 @@ __global__ __launch_bounds__(256) void render_kernel_simple(KParams P, const Dev
     if (COUNT) {
         atomicAdd(&P.counters[0], (unsigned long long)tests);
         atomicAdd(&P.counters[1], (unsigned long long)iters);
+        if (mism) atomicAdd(&P.counters[2], (unsigned long long)mism);
     }
 }
 
@@ -176,6 +179,7 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P, const DevScene* 
     smp.g = P.g;
     smp.cnt.tests = 0;
     smp.cnt.iterations = 0;
+    smp.cnt.draw_mismatch = 0;
 
     while (true) {
         /* (1) converged: lanes without a pixel take the next ones from the queue */
@@ -361,7 +365,7 @@ __global__ void phase_probe_kernel(double g, double dx, double dy, double dz, co
         Sampler<false> smp;
         smp.X = X[i];
         smp.g = g;
-        smp.cnt.tests = smp.cnt.iterations = 0;
+        smp.cnt.tests = smp.cnt.iterations = smp.cnt.draw_mismatch = 0;
         const dv3 w = phase_sample(smp, din);
         dirs[3 * i] = w.x;
         dirs[3 * i + 1] = w.y;
@@ -895,7 +899,7 @@ int vpt_count_work(vpt_context* ctx, const vpt_params* p, uint64_t* tests, uint6
     HIP_OK(hipMalloc(&d, bytes));
     K.out = d;
     K.counters = ctx->d_counters;
-    unsigned long long hc[2] = {0, 0};
+    unsigned long long hc[3] = {0, 0, 0};
     hipError_t e = hipMemset(ctx->d_counters, 0, sizeof hc);
     if (e == hipSuccess) {
         rc = launch_render<true>(ctx, K, nullptr);
@@ -904,6 +908,9 @@ int vpt_count_work(vpt_context* ctx, const vpt_params* p, uint64_t* tests, uint6
     (void)hipFree(d);
     if (rc) return rc;
     if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_count_work: %s", hipGetErrorString(e));
+    if (hc[2])  /* the kill-predicting rings would lose bit-exactness on this scene (vpt_pool.h) */
+        return vpt_fail(VPT_E_INTERNAL, "vpt_count_work: %llu events drew a different number of samples than the "
+                        "kill prediction assumes", (unsigned long long)hc[2]);
     if (tests) *tests = hc[0];
     if (iterations) *iterations = hc[1];
     return VPT_OK;
@@ -1143,6 +1150,9 @@ extern "C" int vpt_debug_set_launch_bound(vpt_context* ctx, int log2)
 /* debug, host only (no GPU): the launches a pool render of p's shard makes on `blocks` workgroups with the
  * bound 2^log2 -- the same units (tiles of 8 x 8 pixels x chunks, vpt_chunks.h) and the same split as
  * launch_pool.  Writes up to cap (unit0, nunits) pairs; returns the number of launches, or < 0. */
+/* debug: task slots per workgroup pool of this build (vpt_pool.h POOL) */
+extern "C" int vpt_debug_pool_tasks(void) { return POOL; }
+
 extern "C" int64_t vpt_debug_launch_plan(const vpt_params* p, int blocks, int log2, uint64_t* unit0, uint64_t* nunits,
                                          int64_t cap)
 {
@@ -1152,6 +1162,9 @@ extern "C" int64_t vpt_debug_launch_plan(const vpt_params* p, int blocks, int lo
     const int chunk = p->chunk_spp > 0 ? (p->chunk_spp < p->spp ? p->chunk_spp : p->spp) : vpt_auto_chunk(p->spp);
     const vpt_chunk_layout lay = vpt_chunks(p->spp, chunk, p->chunk_spp == 0);
     const uint64_t units = (uint64_t)((p->width + 7) / 8) * (uint64_t)((rows + 7) / 8) * 64u * (uint64_t)lay.n;
+    /* launch_pool's clamp: no more workgroups than the units fill (one pool of POOL tasks each) */
+    const uint64_t need = (units + POOL - 1) / POOL;
+    if ((uint64_t)blocks > need) blocks = (int)need;
     const uint64_t max_units = launch_max_units(blocks, lay.C, log2);
     int64_t k = 0;
     for (uint64_t u0 = 0; u0 < units; u0 += max_units, ++k) {

@@ -55,6 +55,15 @@ namespace vpt {
 #ifndef VPT_KILL_RINGS
 #define VPT_KILL_RINGS 1
 #endif
+#ifndef VPT_FUSE_CONT
+#define VPT_FUSE_CONT 0     /* the continuation ray in the event's own intersection pass (ContHit, vpt_device.h); A/B r05: slower, see DESIGN */
+#endif
+#ifndef VPT_MERGE_KINDS
+/* surface (diffuse) and medium events compiled once for both light kinds -- the ring still fixes the
+ * kind for a whole batch, so its branches are wave-uniform -- instead of once per kind: the hot code
+ * is what the shared 64 KB instruction cache has to hold (round 5: I-cache misses track code size) */
+#define VPT_MERGE_KINDS 1
+#endif
 #ifndef VPT_SCHED_PRIO
 #define VPT_SCHED_PRIO 3    /* s_setprio level of the scheduler's critical section (0: off; A/B 3 vs 0: +0.7 %) */
 #endif
@@ -220,6 +229,8 @@ __device__ __forceinline__ dv3 pool_camera_dir(const PoolParams& P, double jx, d
 struct Task {
     Path p;
     Event e;
+    ContHit pre;     /* the continuation ray's nearest hit, when the event's pass found it (registers only) */
+    bool have_pre;
     dv3 acc;
     uint64_t X;
     uint64_t key;    /* the unit's pixel stream key */
@@ -310,16 +321,24 @@ __device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sample
             st = st < R_MD ? st - R_SD + R_S : st - R_MD + R_M;
         }
         /* metal (R_S + 2) and other materials (R_S + 3) are rare: 1.4 % of surface events at the
-         * bench scene */
+         * bench scene.  A diffuse or medium event of a path that continues casts its continuation ray
+         * in its own pass over the spheres (ContHit, VPT_FUSE_CONT); stage A's decide() then visits
+         * no sphere for these lanes. */
+        constexpr bool FUSE = VPT_FUSE_CONT && !COUNT && (EST == 0 || EST == 1 || EST == 2 || EST == 4);
+        ContHit* ch = FUSE && cont ? &t.pre : nullptr;
         if (st < R_M) {
-            if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m, cont);
-            else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m, cont);
+            if (VPT_MERGE_KINDS && st < R_S + 2) {  /* one copy for both light kinds, kind = the ring */
+                surface_event<EST, COUNT, 0, -1>(S, smp, t.p, t.e, m, cont, ch, st - R_S);
+            } else if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m, cont, ch);
+            else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m, cont, ch);
             else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
             else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
-        } else if (st == R_M) {
-            medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m, cont);
+            t.have_pre = FUSE && cont && st < R_S + 2 && S->n_mis == 2;
         } else {
-            medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m, cont);
+            if (VPT_MERGE_KINDS) medium_event<EST, COUNT, -1>(S, smp, t.p, t.e, m, cont, ch);
+            else if (st == R_M) medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m, cont, ch);
+            else medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m, cont, ch);
+            t.have_pre = FUSE && cont;
         }
         SECT_END(ev, st < R_M ? SECT_S_TOTAL : SECT_M_TOTAL);
         SECT_BEGIN(cp);
@@ -360,6 +379,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         t.acc = add(t.p.L, t.acc);  /* src/rt.cpp:794 */
         t.in_path = false;
         t.killed = false;
+        t.have_pre = false;        /* (its continuation ray is never cast) */
     }
     const unsigned long long c0 = dbg_clock(dbg);
     SECT_BEGIN(pr);
@@ -495,6 +515,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         t.p.depth = 0;
         if (EST == 5) t.e.pdf = 1;  /* iterativePathTracer's `factor` rides in the event's pdf slot */
         t.X = smp.X;
+        t.have_pre = false;
         SECT_END(ci, SECT_A_CAMERA_IN);
     }
     SECT_END(cam, SECT_A_CAMERA);
@@ -504,7 +525,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
     if (!done && !parked) {
         SECT_BEGIN(dci);
         smp.X = t.X;
-        const int ev = decide<EST>(S, smp, t.p, t.e, m);
+        const int ev = decide<EST>(S, smp, t.p, t.e, m, t.have_pre, t.pre);
         t.X = smp.X;
         if (ev == EV_END) {
             t.acc = add(t.p.L, t.acc);
@@ -560,6 +581,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
     smp.g = m.g;
     smp.cnt.tests = 0;
     smp.cnt.iterations = 0;
+    smp.cnt.draw_mismatch = 0;
     int n = 0, slot = 0, next = R_A;
     unsigned long long st_idle = 0, st_retry = 0, st_sched = 0, st_b[NR] = {}, st_l[NR] = {}, st_c[3] = {};
     ADbg D = {};
@@ -711,6 +733,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         /* one copy of stage A in the code: a batch of ring A runs it alone, a batch of an S/M ring
          * runs its event first and then stage A on the same lanes */
         SECT_BEGIN(ld);
+        t.have_pre = false;
         if (active) load_task(sh, slot, t, true);
         else {
             t.c1 = 0;

@@ -8,7 +8,7 @@ name=$1
 shift
 mkdir -p build_variants
 C=minimal_volumetric_path_tracer_amd/csrc
-flock /tmp/vpt_build_variant.lock make -s -C "$C" vpt_host.o vpt_multi.o
+flock /tmp/vpt_build_variant.lock make -s -C "$C" vpt_host.o vpt_multi.o  # (the in-tree make takes the same lock: scripts/build_main.sh)
 # the Makefile's flags (SCHED: the scheduler strategy; SCHED= builds with the compiler's default)
 SCHED=${SCHED--mllvm -amdgpu-sched-strategy=iterative-maxocc}
 FLAGS="--offload-arch=${VARCH:-gfx950} -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $SCHED -Wno-unused-function $*"

@@ -4,8 +4,10 @@
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-P1="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS"
-P2="TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCC_EA0_WRREQ_sum"
+P1=${P1:-"SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS"}
+P2=${P2:-"TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCC_EA0_WRREQ_sum"}
+# the timed dispatch only (bench.py runs the counting build, pool_kernel<EST, true>, first)
+export PMC_KERNEL=${PMC_KERNEL:-"pool_kernel<0, false>"}
 for v in "$@"; do
     lib=build_variants/libvpt_$v.so
     [ "$v" = base ] && lib=minimal_volumetric_path_tracer_amd/libvpt.so
@@ -18,16 +20,16 @@ for v in "$@"; do
         if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmcv_${v}_p$i.log; echo "STOP rc=$rc"; exit $rc; fi
     done
     python3 - "$v" <<'PY'
-import csv, glob, sys, collections
+import csv, glob, os, sys, collections
 v = sys.argv[1]
 acc, dur = collections.defaultdict(float), []
 for p in glob.glob(f"gpurun_out/pmcv_{v}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(p)):
-        if "pool_kernel" in r["Kernel_Name"]:
+        if os.environ["PMC_KERNEL"] in r["Kernel_Name"]:
             acc[r["Counter_Name"]] += float(r["Counter_Value"])
 for p in glob.glob(f"gpurun_out/pmcv_{v}/p1/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(p)):
-        if "pool_kernel" in r["Kernel_Name"]:
+        if os.environ["PMC_KERNEL"] in r["Kernel_Name"]:
             dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
 print(f"{v}: pool_kernel ms {dur}  " + "  ".join(f"{k} {acc[k]:.4g}" for k in sorted(acc)))
 print(f"   waitany/wave_cycles {acc['SQ_WAIT_ANY'] / max(1, acc['SQ_WAVE_CYCLES']):.3f}")

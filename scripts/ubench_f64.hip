@@ -63,13 +63,12 @@ int main()
 {
     double* d;
     hipMalloc(&d, 256 * 1024 * sizeof(double));
-    for (int w = 1; w <= 4; w *= 2) {
-        run<4, 0>("fma64", d, w);
-        run<4, 4>("fma64k2", d, w);
-        run<4, 5>("fma64k1", d, w);
-        run<8, 4>("fma64k2", d, w);
-    }
+    /* dependent-chain latency (1 chain, 1 wave/SIMD) vs issue rate (many chains, 2 waves/SIMD) */
     for (int w = 1; w <= 2; w *= 2) {
+        run<1, 0>("fma64", d, w);
+        run<2, 0>("fma64", d, w);
+        run<4, 0>("fma64", d, w);
+        run<8, 0>("fma64", d, w);
         run<1, 1>("mul64", d, w);
         run<4, 1>("mul64", d, w);
         run<1, 2>("rsq64", d, w);
@@ -77,5 +76,7 @@ int main()
         run<1, 3>("fma32", d, w);
         run<4, 3>("fma32", d, w);
     }
+    run<1, 0>("fma64", d, 4);
+    run<4, 0>("fma64", d, 4);
     return 0;
 }

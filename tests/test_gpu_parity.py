@@ -49,6 +49,40 @@ def test_device_math_bitwise(gpu_tracer, orc, orc_vm, fn, lo, hi):
         assert same.all(), f"fn {fn}: {(~same).sum()} differ, e.g. x={x[~same][:3]} dev={dev[~same][:3]} host={host[~same][:3]}"
 
 
+def test_device_tan_range_boundaries(gpu_tracer, orc):
+    """gm_tan on the device over the ranges the [-1.5, 1.5] sweep above leaves out: [1.5,
+    pi/2) -- the odd-n branch where -1/y goes through the double-double division, reached by the
+    equi-angular sampler's tan near +-pi/2 -- and (0.787, 25] after the reduction by pi/2; plus the CPU
+    test's range bounds and table-node boundaries (tests/test_glibc_libm.py::test_tan_range_boundaries),
+    against glibc's tan bit for bit"""
+    rng = np.random.default_rng(306)
+    nodes = (np.arange(0, 190) + 15.5) / 256
+    bounds = np.array([float.fromhex(h) for h in ("0x1.b096cp-27", "0x1.f212dp-5", "0x1.92f1ap-1")] + [25.0])
+    x = np.concatenate([nodes, np.pi / 2 - nodes, np.pi / 2 + nodes, bounds, np.nextafter(bounds, 0),
+                        np.nextafter(bounds, 1), np.pi / 4 * np.arange(-31, 32), rng.uniform(1.5, np.pi / 2, 100_000),
+                        np.pi / 2 - np.exp(rng.uniform(-40, -3, 20_000)), rng.uniform(0.787, 25.0, 100_000)])
+    x = np.concatenate([x, -x])
+    got, want = gpu_tracer.math_probe(5, x), orc.math(5, x)
+    same = bitwise_equal(got, want)
+    assert same.all(), f"{(~same).sum()} of {len(x)} differ, e.g. x={x[~same][:4]}"
+
+
+@pytest.mark.parametrize("est", ["ff", "mis", "explicit_free", "explicit"])
+def test_kill_prediction_draw_counts(gpu_tracer, est):
+    """the pool's kill-predicting rings (vpt_pool.h) assume a diffuse surface event draws 2 n_mis + 4
+    samples and a medium event 4 before the next roulette draw; vpt_count_work's counting kernel checks
+    that on every event it traces and fails (VPT_E_INTERNAL) otherwise -- over the test and
+    alternate scenes, with HG and a depth cap"""
+    from scenes import ALT_SCENES, EST_SCENES
+
+    for name, mk in list(EST_SCENES.items()) + list(ALT_SCENES.items()):
+        gpu_tracer.set_scene(mk())
+        for kw in ({}, dict(hg_g=0.5), dict(max_depth=3)):
+            tests, iters = gpu_tracer.count_work(vpt.RenderConfig(width=24, height=16, spp=8, estimator=est, **kw))
+            assert tests > 0 and iters > 0, (name, kw)
+    gpu_tracer.set_scene(vpt.default_scene())
+
+
 def test_device_sqrt_div_correctly_rounded(gpu_tracer, orc):
     rng = np.random.default_rng(5)
     x = np.abs(rng.normal(size=300000)) * 10.0 ** rng.integers(-300, 300, 300000)
@@ -490,7 +524,7 @@ def _set_launch_bound(tracer, log2):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("w,h,spp,log2,est,kw", [
-    # 7 launches of 1664 units, the last one 1280 (tests/test_launch_plan.py)
+    # 7 launches of 1792 units, the last one 512, at the 14 workgroups launch_pool clamps it to (tests/test_launch_plan.py)
     (32, 32, 96, 12, "ff", {}),
     (32, 32, 96, 12, "mis", dict(hg_g=0.5)),
     # configs[4]'s layout: 8192 spp -> 64-sample chunks + taper (137 chunks), split into 4 launches

@@ -20,6 +20,18 @@ def _plan_fn():
     return f
 
 
+def pool_tasks() -> int:
+    """task slots per workgroup of this build (vpt_pool.h POOL): 856 with the 11 kill-predicting rings"""
+    f = vpt.lib().vpt_debug_pool_tasks
+    f.restype = ctypes.c_int
+    return int(f())
+
+
+def clamped(blocks: int, units: int) -> int:
+    """launch_pool's workgroup count: no more pools than the units fill"""
+    return min(blocks, -(-units // pool_tasks()))
+
+
 def plan(cfg: vpt.RenderConfig, blocks: int, log2: int = 26):
     f = _plan_fn()
     p = cfg.params()
@@ -79,22 +91,24 @@ def test_lowered_bound_splits_into_contiguous_launches(w, h, spp, blocks, log2):
     units, C = units_of(w, h, spp)
     u0, nu = plan(cfg, blocks=blocks, log2=log2)
     _check_partition(u0, nu, units)
-    per = max(1, (2 ** log2 * blocks) // C)
+    per = max(1, (2 ** log2 * clamped(blocks, units)) // C)
     assert nu[0] == min(per, units) and len(nu) == -(-units // per)
 
 
 def test_gpu_split_test_geometry_splits():
     """the GPU test's render (tests/test_gpu_parity.py::test_split_launches_equal_one_launch) takes >= 3
-    launches for any workgroup count it can get, and 7 with a partial last one at the 13 workgroups
-    launch_pool gives it (its units / the 880-task pool)"""
-    units, _ = units_of(32, 32, 96)
-    assert -(-units // 880) == 13
-    for blocks in range(1, 14):
+    launches for any workgroup count it can get, and at the count launch_pool clamps it to (its units
+    over one pool, vpt_debug_pool_tasks) the plan ends in a partial launch"""
+    units, C = units_of(32, 32, 96)
+    full = -(-units // pool_tasks())
+    assert pool_tasks() == 856 and full == 14
+    for blocks in range(1, full + 3):
         u0, nu = plan(vpt.RenderConfig(width=32, height=32, spp=96), blocks=blocks, log2=12)
         _check_partition(u0, nu, units)
         assert len(nu) >= 3
-        if blocks == 13:  # what launch_pool takes on any GPU with >= 13 CUs
-            assert len(nu) == 7 and nu[-1] < nu[0]
+        if blocks >= full:  # what launch_pool takes on any GPU with >= 14 CUs: 7 launches, the last partial
+            per = (2 ** 12 * full) // C
+            assert nu[0] == per and len(nu) == -(-units // per) == 7 and nu[-1] == units - 6 * per < per
 
 
 def test_bad_arguments_refused():
