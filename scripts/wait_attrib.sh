@@ -7,10 +7,10 @@
 set -u
 TAG=${1:?tag}
 export PMC_TIMEOUT=${PMC_TIMEOUT:-240}
-export PMC_PASSES="VmemLatency SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAVE_CYCLES SQ_WAIT_ANY;\
-SmemLatency SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_INST_CYCLES_SMEM SQ_INST_CYCLES_VMEM_RD;\
-LdsLatency SQ_WAVE_CYCLES SQ_WAIT_INST_LDS;\
-InstrFetchLatency SQ_WAVE_CYCLES SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_BUSY_CYCLES;\
+export PMC_PASSES="VmemLatency SQ_INSTS_VMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAVE_CYCLES SQ_WAIT_ANY;\
+SmemLatency SQ_INSTS_SMEM_NORM SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_INST_CYCLES_SMEM SQ_INST_CYCLES_VMEM_RD;\
+LdsLatency SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_LDS;\
+InstrFetchLatency SQ_IFETCH SQ_WAVE_CYCLES SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_BUSY_CYCLES;\
 SQC_DCACHE_MISSES SQC_DCACHE_HITS SQC_DCACHE_REQ SQ_WAVE_CYCLES TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum"
 bash scripts/pmc.sh "$TAG" --steps 1 --warmup 0 --no-cpu --inflight 1 || exit $?
 mkdir -p gpurun_out/wait_$TAG
