@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # PMC of the pool kernel for libvpt.so variants (build_variants/libvpt_<name>.so; "base" = in-tree):
-# two short passes each (one FF bench step), summarised per variant.  usage: bash scripts/pmc_var.sh name...
+# two short passes each (one FF bench step; PMCV_ARGS= also runs the north-star MIS + HG step, for
+# PMC_KERNEL="pool_kernel<1, false>"), summarised per variant.  usage: bash scripts/pmc_var.sh name...
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -15,7 +16,7 @@ for v in "$@"; do
     for p in "$P1" "$P2"; do
         i=$((i + 1))
         VPT_LIB=$lib timeout -k 10 300 rocprofv3 --pmc $p --kernel-trace -d gpurun_out/pmcv_$v/p$i -o run --output-format csv -- \
-            python3 bench.py --steps 1 --warmup 0 --no-cpu --inflight 1 --no-north-star > gpurun_out/pmcv_${v}_p$i.log 2>&1
+            python3 bench.py --steps 1 --warmup 0 --no-cpu --inflight 1 ${PMCV_ARGS---no-north-star} > gpurun_out/pmcv_${v}_p$i.log 2>&1
         rc=$?
         if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmcv_${v}_p$i.log; echo "STOP rc=$rc"; exit $rc; fi
     done
