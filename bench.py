@@ -264,10 +264,13 @@ def cpu_baseline(img: np.ndarray, c: dict, threads: int) -> dict:
                             "how": f"EXTRAPOLATION, not a measurement: measured {len(cpus)}-core rate x {S}/{len(cpus)} "
                                    f"(the per-thread flavour has no shared state; the job's CPU share is {len(cpus)} "
                                    f"cores, not the socket, so the other {S - len(cpus)} cores cannot be run)"},
+        # the FASTEST of the three runs of each: a run slowed by the box's other tenants can only lower
+        # this figure's ratio, never raise it
         "socket_estimate_conservative": {
-            "value": max(v_n * S / len(cpus), v_1 * S),
-            "how": f"max({len(cpus)}-core median x {S}/{len(cpus)}, one-core median x {S}): the socket at no worse than "
-                   f"perfect scaling of one core"},
+            "value": max(px * spp_n / min(runs_n) / 1e6 * S / len(cpus), px * spp_1 / min(runs_1) / 1e6 * S),
+            "how": f"max(fastest {len(cpus)}-core run x {S}/{len(cpus)}, fastest one-core run x {S}) of the three "
+                   f"runs each: the socket at no worse than perfect scaling of one core, with host noise only ever "
+                   f"lowering the ratio"},
         "as_written": {"value": v_a, "kind": "reference",
                        "sample": f"oracle/_ref/rt (src/rt.cpp unchanged: one erand48 state shared by all threads, "
                                  f"SURVEY H4), `rt {spp_a}`, {len(cpus)} threads on the same cores, {el_a:.2f}s"},
@@ -707,7 +710,8 @@ def main() -> None:
                 misn["runs"] = [round(r["value"], 3) for r in runs]
                 S = cb["socket_physical_cores"]
                 sock = misn["value"] * S / misn["cores"]
-                sock_c = max(sock, mis1 * S)
+                # fastest of the three runs of each (host noise can only lower the conservative ratio)
+                sock_c = max(max(r["value"] for r in runs) * S / misn["cores"], max(one) * S)
                 o["cpu_reference"] = {"measured": misn, "one_core": mis1, "one_core_runs": [round(x, 4) for x in one],
                                       "parallel_efficiency": misn["value"] / (mis1 * misn["cores"]),
                                       "socket_estimate": sock,
@@ -715,8 +719,9 @@ def main() -> None:
                                       "how": f"reference MISVPTTracerRecursive (oracle/_ref/libvpt_ref.so) measured on "
                                              f"{misn['cores']} cores x {S}/{misn['cores']}: an EXTRAPOLATION to the "
                                              f"{S}-core socket (the job has {misn['cores']} cores, not the socket); the "
-                                             f"conservative estimate is max(that, one-core median x {S}), i.e. never "
-                                             f"below perfect scaling of one core",
+                                             f"conservative estimate is max(fastest {misn['cores']}-core run x "
+                                             f"{S}/{misn['cores']}, fastest one-core run x {S}) over the three runs "
+                                             f"each, i.e. never below perfect scaling of one core",
                                       "phase": "the CPU side runs the reference's ISOTROPIC phase (it has no HG); the "
                                                "GPU side runs HG g=0.5 (the north-star extension, g=0 reduces to "
                                                "the reference bit for bit)"}

@@ -181,6 +181,41 @@ struct PoolParams {
     unsigned* queue;
 };
 
+/* VPT_P_KARG: the launch parameters read where they are used, by scalar loads from the kernel-argument
+ * segment through an opaque pointer (the kernel's first argument sits at offset 0), instead of held
+ * in SGPRs for the whole kernel: the unit hand-out, camera, partial-store and refill blocks use them
+ * once per batch or less. */
+#ifndef VPT_P_KARG
+#define VPT_P_KARG 1
+#endif
+#if VPT_P_KARG && defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) PoolParams PoolParamsK;
+__device__ __forceinline__ PoolParamsK& pool_params_at_use()
+{
+    uint64_t a = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    __asm__ volatile("" : "+s"(a));
+    return *(PoolParamsK*)a;
+}
+#define VPT_PARAMS(Pin) PoolParamsK& P = pool_params_at_use(); (void)(Pin)
+#else
+#define VPT_PARAMS(Pin) const PoolParams& P = (Pin)
+#endif
+
+/* vpt_chunk_of_end / vpt_chunk_range on a copy of the layout (the parameters may sit in the constant
+ * address space, VPT_P_KARG) */
+template <class LAY>
+__device__ __forceinline__ int vpt_chunk_of_end_lay(const LAY& lay, int c1)
+{
+    const vpt_chunk_layout l = lay;
+    return vpt_chunk_of_end(&l, c1);
+}
+template <class LAY>
+__device__ __forceinline__ void vpt_chunk_range_lay(const LAY& lay, int c, int* s0, int* s1)
+{
+    const vpt_chunk_layout l = lay;
+    vpt_chunk_range(&l, c, s0, s1);
+}
+
 /* a / d for a launch constant d = 2^sh (sh >= 0: a shift; the branch is uniform) */
 __device__ __forceinline__ unsigned udiv_p(unsigned a, unsigned d, int sh) { return sh >= 0 ? a >> sh : a / d; }
 
@@ -192,8 +227,9 @@ struct Unit {
     bool valid;
 };
 
-__device__ __forceinline__ Unit decode_unit(const PoolParams& P, unsigned u)
+__device__ __forceinline__ Unit decode_unit(const PoolParams& P0, unsigned u)
 {
+    VPT_PARAMS(P0);
     u += P.unit0;
     Unit r;
     const unsigned c = udiv_p(u, P.level_units, P.sh_lu), rem = u - c * P.level_units;
@@ -210,8 +246,9 @@ __device__ __forceinline__ Unit decode_unit(const PoolParams& P, unsigned u)
 }
 
 /* camera ray through pixel (x, y) with jitter (jx, jy) -- src/rt.cpp:787-789 */
-__device__ __forceinline__ dv3 pool_camera_dir(const PoolParams& P, double jx, double jy, int x, int y)
+__device__ __forceinline__ dv3 pool_camera_dir(const PoolParams& P0, double jx, double jy, int x, int y)
 {
+    VPT_PARAMS(P0);
     const dv3 cd = mk(P.d[0], P.d[1], P.d[2]);
     const dv3 cx = mk(P.cx[0], P.cx[1], P.cx[2]), cy = mk(P.cy[0], P.cy[1], P.cy[2]);
     const double ux = (double)x + jx - 0.5, uy = (double)y + jy - 0.5;
@@ -288,14 +325,15 @@ __device__ __forceinline__ void store_task(TaskPool& sh, int s, const Task& t, b
 }
 
 /* the finished unit's chunk sum -> partials[chunk][shard row][x] */
-__device__ __forceinline__ void store_partial(const PoolParams& P, const Task& t)
+__device__ __forceinline__ void store_partial(const PoolParams& P0, const Task& t)
 {
+    VPT_PARAMS(P0);
     const int x = (int)(t.pix & 0xFFFFu), y = (int)(t.pix >> 16);
     const int fr = P.h - 1 - y;
     const int k = (int)udiv_p((unsigned)fr, (unsigned)P.band_rows, P.sh_br), rr = fr - k * P.band_rows;
     const int lr = (int)udiv_p((unsigned)(k - P.band_offset), (unsigned)P.band_stride, P.sh_bs) * P.band_rows + rr;
     const int c = (int)t.c1 <= P.lay.head ? (int)udiv_p(t.c1 - 1u, (unsigned)P.lay.C, P.sh_c)  /* vpt_chunk_of_end */
-                                          : vpt_chunk_of_end(&P.lay, (int)t.c1);
+                                          : vpt_chunk_of_end_lay(P.lay, (int)t.c1);
     const size_t o = (((size_t)c * (size_t)P.rows + (size_t)lr) * (size_t)P.w + (size_t)x) * 3;
     P.partials[o] = t.acc.x;
     P.partials[o + 1] = t.acc.y;
@@ -370,10 +408,11 @@ __device__ __forceinline__ bool path_ends_after_event(uint64_t X, int depth, con
  * that ends there goes back to ring A.  Returns the ring of the task's next stage (R_DONE:
  * retired). */
 template <int EST, bool COUNT>
-__device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const DevScene* __restrict__ S,
+__device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P0, const DevScene* __restrict__ S,
                                        const Medium& m, Sampler<COUNT>& smp, Task& t, bool active, int lane,
                                        uint64_t below, bool dbg, ADbg& D)
 {
+    VPT_PARAMS(P0);
     bool done = !active, parked = false, fresh = false;
     if (active && t.killed) {  /* the S/M roulette ended the path */
         t.acc = add(t.p.L, t.acc);  /* src/rt.cpp:794 */
@@ -437,7 +476,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                     if (ex) done = true;
                     else parked = true;
                 } else {
-                    const Unit uu = decode_unit(P, ent);
+                    const Unit uu = decode_unit(P0, ent);
                     if (uu.valid) {  /* (an invalid unit -- a tile's padding -- is dropped) */
                         t.pix = (unsigned)uu.x | ((unsigned)uu.y << 16);
                         t.key = vpt_stream_key(P.seed, (uint64_t)(P.h - 1 - uu.y) * (uint64_t)P.w + (uint64_t)uu.x);
@@ -446,7 +485,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                             s0 = uu.c * P.lay.C;
                             s1 = s0 + P.lay.C < P.lay.head ? s0 + P.lay.C : P.lay.head;
                         } else {
-                            vpt_chunk_range(&P.lay, uu.c, &s0, &s1);
+                            vpt_chunk_range_lay(P.lay, uu.c, &s0, &s1);
                         }
                         t.i = (unsigned)s0;
                         t.c1 = (unsigned)s1;
@@ -483,7 +522,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
                 }
             }
             if (VPT_UNLIKELY(!t.in_path && t.i == t.c1)) {  /* the unit is done: its chunk sum out */
-                store_partial(P, t);
+                store_partial(P0, t);
                 t.c1 = 0;
             }
         }
@@ -509,7 +548,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
         const double jy = smp.next();
         if (EST != 5) (void)smp.next();  /* the roulette draw, decided above */
         t.p.o = mk(P.o[0], P.o[1], P.o[2]);
-        t.p.d = pool_camera_dir(P, jx, jy, (int)(t.pix & 0xFFFFu), (int)(t.pix >> 16));
+        t.p.d = pool_camera_dir(P0, jx, jy, (int)(t.pix & 0xFFFFu), (int)(t.pix >> 16));
         t.p.beta = mk(1, 1, 1);
         t.p.L = mk(0, 0, 0);
         t.p.depth = 0;
@@ -561,7 +600,7 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P, const 
 }
 
 template <int EST, bool COUNT>
-__global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(PoolParams P, Medium m, const DevScene* __restrict__ S,
+__global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(PoolParams P0, Medium m0, const DevScene* __restrict__ S,
                                                    unsigned long long* counters, unsigned long long* stats)
 {
     __shared__ TaskPool sh;
@@ -578,7 +617,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
 
     Sampler<COUNT> smp;
     smp.X = 0;
-    smp.g = m.g;
+    smp.g = m0.g;
     smp.cnt.tests = 0;
     smp.cnt.iterations = 0;
     smp.cnt.draw_mismatch = 0;
@@ -626,6 +665,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                 if (__builtin_amdgcn_readfirstlane(own)) {
                     const int t0 = __builtin_amdgcn_readfirstlane(lds_peek(&sh.ctl[C_UTAIL]));
                     if (t0 - __builtin_amdgcn_readfirstlane(lds_peek(&sh.ctl[C_UHEAD])) < UREFILL) {
+                        VPT_PARAMS(P0);
                         unsigned ubase = 0;
                         if (lane == 0) ubase = atomicAdd(P.queue, (unsigned)UREFILL);
                         ubase = (unsigned)__builtin_amdgcn_readfirstlane((int)ubase);
@@ -727,6 +767,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         }
 
         /* ---- run one stage on the batch ---- */
+        const Medium& m = m0;
         const bool active = lane < n;
         Task t;
         const int stage = st == R_A ? 0 : st < R_M ? 1 : 2;
@@ -746,7 +787,7 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
             run_event<EST, COUNT>(S, smp, t, m, st);
             t.X = smp.X;
         }
-        next = stage_a<EST>(sh, P, S, m, smp, t, active, lane, below, dbga, D);
+        next = stage_a<EST>(sh, P0, S, m, smp, t, active, lane, below, dbga, D);
         SECT_BEGIN(stt);
         if (active) store_task(sh, slot, t, true);
         SECT_END(stt, SECT_STORE);

@@ -20,6 +20,7 @@ ARMS = {
     "pool_stats": ["-DVPT_POOL_DEBUG=1"],
     "pool_timeline": ["-DVPT_POOL_DEBUG=2"],
     "debug_env": ["-DVPT_DEBUG_ENV=1"],
+    "params_in_sgprs": ["-DVPT_P_KARG=0"],  # launch parameters held for the whole kernel (pre-round-5 form)
 }
 
 
