@@ -604,6 +604,11 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
                                                    unsigned long long* counters, unsigned long long* stats)
 {
     __shared__ TaskPool sh;
+#if VPT_P_KARG && defined(__HIP_DEVICE_COMPILE__)
+    /* pool_params_at_use() reads P0 at offset 0 of the argument segment: P0 must stay the first argument
+     * (if it moves, the launch renders nothing and every parity test fails) */
+    if (pool_params_at_use().nunits != P0.nunits || pool_params_at_use().unit0 != P0.unit0) return;
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     for (int j = tid; j < POOL; j += VPT_POOL_THREADS) {
