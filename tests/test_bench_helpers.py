@@ -72,3 +72,14 @@ def test_reference_estimator_rate_multiprocess():
     r = bench.reference_estimator_rate(1, c, cpus, rows_per=2, spp=4)
     assert r["cores"] == len(cpus) and r["value"] > 0
     assert f"{len(cpus)} processes" in r["sample"]
+
+
+def test_socket_conservative_uses_the_fastest_runs():
+    """the conservative socket figure (the denominator of the quoted GPU/CPU ratios) takes the fastest run
+    of each set, so a slow outlier lowers the ratio, never raises it; and it is never below one core x 64"""
+    # 16-core runs 18, 20, 22 Msamples/s; one-core 1.1, 1.3, 1.2
+    assert bench.socket_conservative([18.0, 20.0, 22.0], [1.1, 1.3, 1.2], 16, 64) == max(22.0 * 4, 1.3 * 64)
+    # poor 16-core scaling: the one-core figure decides
+    assert bench.socket_conservative([12.0, 13.0, 11.0], [1.3, 1.25, 1.2], 16, 64) == 1.3 * 64
+    # a slowed run cannot raise the ratio: adding a slower run leaves the figure unchanged
+    assert bench.socket_conservative([22.0, 10.0], [1.3, 0.5], 16, 64) == bench.socket_conservative([22.0], [1.3], 16, 64)
