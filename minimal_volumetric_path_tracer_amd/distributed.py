@@ -37,6 +37,20 @@ def shard_rows(height: int, rank: int, world: int, band_rows: int = DEFAULT_BAND
     return [fr for b in range(rank, nb, world) for fr in range(b * band_rows, min(height, (b + 1) * band_rows))]
 
 
+_ROW_INDEX: dict = {}
+
+
+def _row_index(height: int, rank: int, world: int, band_rows: int, device) -> Optional[torch.Tensor]:
+    """rank's file rows as an index tensor on `device`, built once per layout: torch.tensor(list,
+    device=gpu) is a blocking copy from pageable memory, which in the per-image gather would make rank 0
+    wait for its own render and serialise the launches the bench keeps in flight"""
+    key = (height, rank, world, band_rows, str(device))
+    if key not in _ROW_INDEX:
+        rows = shard_rows(height, rank, world, band_rows)
+        _ROW_INDEX[key] = torch.tensor(rows, device=device) if rows else None
+    return _ROW_INDEX[key]
+
+
 def assemble(parts: list[torch.Tensor], height: int, band_rows: int = DEFAULT_BAND_ROWS) -> torch.Tensor:
     """Full (height, width, 3) image from the world's strips (parts[r] = rank r's strip)."""
     world = len(parts)
@@ -45,9 +59,9 @@ def assemble(parts: list[torch.Tensor], height: int, band_rows: int = DEFAULT_BA
     width = parts[0].shape[1]
     out = parts[0].new_empty((height, width, 3))
     for r, p in enumerate(parts):
-        rows = shard_rows(height, r, world, band_rows)
-        if rows:
-            out[torch.tensor(rows, device=out.device)] = p[: len(rows)]
+        idx = _row_index(height, r, world, band_rows, out.device)
+        if idx is not None:
+            out[idx] = p[: idx.shape[0]]
     return out
 
 

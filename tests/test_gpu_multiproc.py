@@ -77,3 +77,30 @@ def test_bench_refuses_more_gpus_than_the_box_has():
                        text=True, timeout=120, env=_clean_env(), cwd=ROOT)
     assert r.returncode == 2 and "refusing to run on fewer" in r.stderr, r.stderr[-500:]
     assert not r.stdout.strip()
+
+
+def test_assemble_does_not_block_the_host():
+    """rank 0's per-image reassembly (distributed.assemble, inside bench.py's timed step) enqueues device
+    work only: a blocking host copy there would make rank 0 wait for its own render and serialise the
+    launches the bench keeps in flight (the RCCL runs of the driver's scaling bench go through it)"""
+    import time
+
+    import torch
+
+    from minimal_volumetric_path_tracer_amd.distributed import assemble, shard_rows
+
+    dev = torch.device("cuda:0")
+    H, W, world = 64, 32, 4
+    parts = [torch.full((len(shard_rows(H, r, world)), W, 3), float(r), device=dev) for r in range(world)]
+    first = assemble(parts, H)  # builds the per-layout row indices (once)
+    torch.cuda.synchronize()
+    for r in range(world):
+        assert bool((first[torch.tensor(shard_rows(H, r, world), device=dev)] == r).all())
+    torch.cuda._sleep(200_000_000)  # ~0.1 s of device time queued ahead of the reassembly
+    t0 = time.perf_counter()
+    out = assemble(parts, H)
+    t_host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t_all = time.perf_counter() - t0
+    assert t_host < 0.25 * t_all, (t_host, t_all)
+    assert torch.equal(out, first)
