@@ -76,3 +76,21 @@ def test_assemble_and_shard_configs():
         assert torch.equal(assemble(parts, H, band), full)
         cfg = RenderConfig(width=W, height=H)
         assert sum(shard_config(cfg, r, world, band).shard_rows() for r in range(world)) == H
+
+
+def test_assemble_builds_its_row_indices_once(monkeypatch):
+    """the per-image reassembly on rank 0 reuses its row-index tensors (built on the first image of a
+    layout): building them per image is a blocking host-to-device copy on a GPU rank"""
+    import minimal_volumetric_path_tracer_amd.distributed as d
+
+    full = torch.arange(H * W * 3, dtype=torch.float32).reshape(H, W, 3)
+    world, band = 4, 8
+    parts = [full[shard_rows(H, r, world, band)] for r in range(world)]
+    monkeypatch.setattr(d, "_ROW_INDEX", {})
+    assert torch.equal(assemble(parts, H, band), full)
+    built = dict(d._ROW_INDEX)
+    calls = []
+    real = torch.tensor
+    monkeypatch.setattr(torch, "tensor", lambda *a, **k: calls.append(1) or real(*a, **k))
+    assert torch.equal(assemble(parts, H, band), full)
+    assert calls == [] and d._ROW_INDEX.keys() == built.keys()
