@@ -14,6 +14,9 @@ OUT=gpurun_out/ab_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 lib() { if [ "$1" = base ]; then echo minimal_volumetric_path_tracer_amd/libvpt.so; else echo build_variants/libvpt_$1.so; fi; }
+for v in "$@"; do  # every variant built before any GPU work
+    [ -f "$(lib "$v")" ] || { echo "STOP: $(lib "$v") is missing (scripts/build_variant.sh $v ...)"; exit 2; }
+done
 if [ -z "${NOCHECK:-}" ]; then
     for v in "$@"; do
         VPT_LIB=$(lib "$v") timeout -k 10 240 python scripts/variant_check.py > "$OUT/chk_$v.log" 2>&1
