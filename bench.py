@@ -51,7 +51,7 @@ NORTH_STAR = "mis"          # BASELINE.json configs[2], measured beside the head
 CONFIGS = {
     # BASELINE.json configs[1]
     "ff": dict(width=1024, height=1024, spp=256, estimator="ff", sigma_a=0.001, sigma_s=0.009),
-    # BASELINE.json configs[2] (HG g = 0.5 extension), reduced to fit a quick bench: 1024 spp
+    # BASELINE.json configs[2] at its own size: 1024^2 x 1024 spp, MIS with HG g = 0.5 (the north-star workload)
     "mis": dict(width=1024, height=1024, spp=1024, estimator="mis", sigma_a=0.001, sigma_s=0.009, hg_g=0.5),
     # BASELINE.json configs[3]: dense medium, 8 bounces.  sigma_t 0.03 (3x the default, albedo 0.9 kept):
     # at SURVEY's proposed 0.1 the ~180 units of fog between the camera (z = 214) and the scene pass
@@ -443,15 +443,35 @@ def measure(c: dict, args, tracers, streams, world: int, rank: int, dev) -> dict
             b.record(stream)
         torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    rank_elapsed = [elapsed]
+    gather_ms = None
+    if dist:
+        # the gather alone: all ranks' strips ready (barrier), rank 0's stream timed around the collective
+        # and its copy into the image, serialized, a few times (outside the timed region)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        gts = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(stream):
+                a.record(stream)
+                strip = outs[0] if args.dist_backend == "nccl" else outs[0].cpu()
+                full = gather_image(strip, cfg, band_rows=band)
+                if rank == 0:
+                    images[0].copy_(full)
+                b.record(stream)
+            torch.cuda.synchronize(dev)
+            gts.append(a.elapsed_time(b))
+            dist.barrier()
+        gather_ms = float(np.median(gts))
+    rank_elapsed, rank_kern_ms = [elapsed], [kern_ms]
     if dist:
         tdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=tdev)
         every = [torch.empty_like(t) for _ in range(world)]
         dist.all_gather(every, t)
-        rank_elapsed = [float(x.item()) for x in every]
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the job's time is the slowest rank's
-        elapsed = float(t.item())
+        rank_elapsed = [float(x[0].item()) for x in every]
+        rank_kern_ms = [float(x[1].item()) for x in every]
+        elapsed = max(rank_elapsed)  # the job's time is the slowest rank's
     img = None
     if rank == 0:
         for j in range(1, min(D, args.steps)):  # every slot rendered the same image
@@ -461,13 +481,23 @@ def measure(c: dict, args, tracers, streams, world: int, rank: int, dev) -> dict
     achieved = launch_samples * FLOP_PER_TEST * T / (kern_ms * 1e-3) / 1e12
     return {"value": H * W * SPP * args.steps / elapsed / 1e6, "elapsed": elapsed, "kern_ms": kern_ms, "T": T,
             "achieved": achieved, "launch_samples": launch_samples, "image": img, "band": band, "D": D,
-            "nevents": len(evs), "rank_elapsed": rank_elapsed}
+            "nevents": len(evs), "rank_elapsed": rank_elapsed, "rank_kern_ms": rank_kern_ms, "gather_ms": gather_ms}
 
 
 def workload_name(c: dict) -> str:
     return (f"{c['estimator']} {c['width']}x{c['height']}x{c['spp']}spp default scene, sigma_a {c['sigma_a']} "
             f"sigma_s {c['sigma_s']}" + (f", HG g {c['hg_g']}" if c.get("hg_g") else "")
             + (f", max depth {c['max_depth']}" if c.get("max_depth") else ""))
+
+
+def shared_device_refusal(rank_pci: list, shared_device: bool):
+    """None when every rank has a GPU of its own (distinct PCI ids) or --shared-device declares a test run;
+    otherwise why an N-GPU line must not be printed: N ranks on fewer GPUs would time shared hardware"""
+    if shared_device or len(set(rank_pci)) == len(rank_pci):
+        return None
+    dup = sorted({p for p in rank_pci if rank_pci.count(p) > 1})
+    return (f"refusing a {len(rank_pci)}-GPU line: ranks share GPU(s) {', '.join(dup)}; "
+            "--shared-device marks such a run as a test")
 
 
 def _free_port() -> int:
@@ -498,26 +528,39 @@ def launch_ranks(n: int, cmd: list, env=None, timeout=None) -> int:
         procs.append(subprocess.Popen(cmd, env=e))
     rc, t0 = 0, time.time()
     pending = list(range(n))
-    while pending:
-        for r in list(pending):
-            code = procs[r].poll()
-            if code is None:
-                continue
-            pending.remove(r)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 128 - code
-                print(f"bench.py: rank {r} exited with status {code}; stopping the other ranks", file=sys.stderr)
+    try:
+        while pending:
+            for r in list(pending):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                pending.remove(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {r} exited with status {code}; stopping the other ranks", file=sys.stderr)
+                    for q in pending:
+                        procs[q].terminate()
+            if pending and timeout is not None and time.time() - t0 > timeout:
+                print(f"bench.py: ranks {pending} still running after {timeout}s; stopping them", file=sys.stderr)
                 for q in pending:
-                    procs[q].terminate()
-        if pending and timeout is not None and time.time() - t0 > timeout:
-            print(f"bench.py: ranks {pending} still running after {timeout}s; stopping them", file=sys.stderr)
-            for q in pending:
-                procs[q].kill()
-            rc = rc or 124
-        if pending:
-            time.sleep(0.05)
-    for p in procs:
-        p.wait()
+                    procs[q].kill()
+                rc = rc or 124
+            if pending:
+                time.sleep(0.05)
+    finally:
+        # an exception or ^C in the launcher must not orphan ranks that hold GPUs and a rendezvous:
+        # terminate what still runs, then kill what ignores it (exactly these child PIDs)
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.terminate()
+        t1 = time.time()
+        for p in live:
+            try:
+                p.wait(timeout=max(0.1, 10 - (time.time() - t1)))
+            except subprocess.TimeoutExpired:
+                p.kill()
+        for p in procs:
+            p.wait()
     return rc
 
 
@@ -581,6 +624,23 @@ def main() -> None:
             print(f"bench.py: the process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
             sys.exit(2)
 
+    # what each rank runs on, as the process group reports it (one line per rank, rank order); N ranks on
+    # fewer distinct GPUs than N (a repeated PCI id) cannot give an N-GPU line unless --shared-device says so
+    props = torch.cuda.get_device_properties(dev)
+    pci = f"{getattr(props, 'pci_domain_id', 0):04x}:{getattr(props, 'pci_bus_id', 0):02x}:" \
+          f"{getattr(props, 'pci_device_id', 0):02x}"
+    me = f"rank {rank}: cuda:{dev.index} ({props.name}, PCI {pci})"
+    rank_devices, rank_pci = [me], [pci]
+    if dist:
+        rank_devices, rank_pci = [None] * world, [None] * world
+        dist.all_gather_object(rank_devices, me)
+        dist.all_gather_object(rank_pci, pci)
+    why = shared_device_refusal(rank_pci, args.shared_device)
+    if why:
+        if rank == 0:
+            print(f"bench.py: {why} ({rank_devices})", file=sys.stderr)
+        sys.exit(2)
+
     c = dict(CONFIGS[args.config])
     if args.size:
         w, h, s = (int(v) for v in args.size.lower().split("x"))
@@ -596,14 +656,6 @@ def main() -> None:
     prof = None if args.size else pmc_profile(args.config, world, build)
     full = pmc_fp64_flop(prof)
     kern_ms, T = m["kern_ms"], m["T"]
-    # what each rank ran on, as the process group reports it (one line per rank, rank order)
-    props = torch.cuda.get_device_properties(dev)
-    me = f"rank {rank}: cuda:{dev.index} ({props.name}, PCI {getattr(props, 'pci_domain_id', 0):04x}:" \
-         f"{getattr(props, 'pci_bus_id', 0):02x}:{getattr(props, 'pci_device_id', 0):02x})"
-    rank_devices = [me]
-    if dist:
-        rank_devices = [None] * world
-        dist.all_gather_object(rank_devices, me)
     if rank == 0 and args.save_image:
         np.save(args.save_image, m["image"])
     if rank == 0:
@@ -632,6 +684,11 @@ def main() -> None:
                                   "world_size": dist.get_world_size() if dist else 1,
                                   "rank_devices": rank_devices,
                                   "rank_elapsed_s": [round(x, 6) for x in m["rank_elapsed"]],
+                                  # each rank's serialized launch time of its shard (HIP events on its launch
+                                  # stream) and rank 0's gather of one image's strips, timed serialized after
+                                  # a barrier: imbalance and an exposed gather show here, not in `value`
+                                  "rank_kernel_ms": [round(x, 4) for x in m["rank_kern_ms"]],
+                                  "gather_ms": None if m["gather_ms"] is None else round(m["gather_ms"], 4),
                                   "shared_device": bool(args.shared_device)},
             },
             "roofline": {

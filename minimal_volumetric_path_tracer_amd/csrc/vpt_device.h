@@ -117,6 +117,37 @@ __device__ static inline __attribute__((always_inline)) void sect_flush()
 #define SECT_BEGIN(name) const uint32_t _sect_##name = sect_now()
 #define SECT_END(name, k) sect_add(k, _sect_##name)
 
+/* Differential instruction counts (measurement builds only, scripts/dup_pmc.sh): with -DVPT_DUP=k,
+ * section k (DUP_* below) runs twice -- the first time on opaque copies of its inputs, its results
+ * sunk into an empty asm and discarded -- so the PMC counters of that build minus the release build's
+ * are the section's dynamic instruction counts on the real workload (the same batches, lanes and
+ * branches; the duplicate takes no draw from the task's stream). */
+#ifndef VPT_DUP
+#define VPT_DUP 0
+#endif
+#define DUP_DECIDE 1
+#define DUP_DECIDE_ISECT 2
+#define DUP_SURF 3
+#define DUP_MIS 4
+#define DUP_MIS_ISECT 5
+#define DUP_MED 6
+#define DUP_SS 7
+#define DUP_EQA 8
+#define DUP_PLIGHT 9
+#define DUP_BDSF 10
+#define DUP_PHASE 11
+#define DUP_CAMERA 12
+#define DUP_LDST 13
+#define DUP_SS_ISECT 14
+#define DUP_SS_DIR 15
+#define DUP_MIS_DIRS 16
+__device__ __forceinline__ void vpt_opaque(double& v) { __asm__ volatile("" : "+v"(v)); }
+__device__ __forceinline__ void vpt_opaque(int& v) { __asm__ volatile("" : "+v"(v)); }
+__device__ __forceinline__ void vpt_opaque(uint64_t& v) { __asm__ volatile("" : "+v"(v)); }
+__device__ __forceinline__ void vpt_sink(double v) { __asm__ volatile("" ::"v"(v)); }
+__device__ __forceinline__ void vpt_sink(int v) { __asm__ volatile("" ::"v"(v)); }
+__device__ __forceinline__ void vpt_sink(uint64_t v) { __asm__ volatile("" ::"v"(v)); }
+
 /* ------------------------------------------------------------------ vectors (Vector.h:10-36) */
 struct dv3 {
     double x, y, z;
@@ -128,17 +159,21 @@ VPT_DEV dv3 sub(dv3 a, dv3 b) { return dv3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 VPT_DEV dv3 scl(dv3 a, double s) { return dv3{a.x * s, a.y * s, a.z * s}; }
 VPT_DEV dv3 mul(dv3 a, dv3 b) { return dv3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 VPT_DEV double dot(dv3 a, dv3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+VPT_DEV void vpt_opaque(dv3& a)
+{
+    vpt_opaque(a.x);
+    vpt_opaque(a.y);
+    vpt_opaque(a.z);
+}
+VPT_DEV void vpt_sink(dv3 a)
+{
+    vpt_sink(a.x);
+    vpt_sink(a.y);
+    vpt_sink(a.z);
+}
 VPT_DEV dv3 cross(dv3 a, dv3 b) { return dv3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
-#ifndef VPT_NRM_CALL
-#define VPT_NRM_CALL 0
-#endif
-VPT_DEV dv3 nrm_inl(dv3 a) { return scl(a, vm_inv_sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); }  /* 1.0 / sqrt(|a|^2) */
-#if VPT_NRM_CALL
-/* the reference's normalize out of line: ~100 sites in the pool kernel, ~30 instructions each */
-__device__ static __attribute__((noinline)) dv3 nrm(dv3 a) { return nrm_inl(a); }
-#else
-VPT_DEV dv3 nrm(dv3 a) { return nrm_inl(a); }
-#endif
+/* the reference's normalize, 1.0 / sqrt(|a|^2) times a (inlined: out of line it was slower, round 5) */
+VPT_DEV dv3 nrm(dv3 a) { return scl(a, vm_inv_sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); }
 
 struct Counters {
     uint64_t tests;
@@ -836,33 +871,16 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
     }
 }
 
-/* The next iteration's nearest hit, found inside an event's own intersection pass: the continuation
- * ray leaves the event's vertex, like the event's own rays, so it rides in their pass over the
- * spheres (oc and |oc|^2 formed once) and decide() takes it instead of casting the ray again.  The
- * same operations per sphere as scene_intersect_grouped, in index order: t = tmin (0 on a miss),
- * id unchanged (0) on a miss. */
-struct ContHit {
-    double t;
-    int id;
-    bool hit;
-};
-
 /* MISv2 (include/misSamplingFunctions.h:96-170) for a scene with exactly two MIS lights, same bits
  * and draws as mis_v2: every draw of MISv2 precedes, and none depends on, the three ray casts
  * (the two light samples of muestreoSA, :163-206, and the BSDF sample of uniform / softDielectric
  * / microfacet), so the draws and directions are taken first in the reference's order, the three
  * rays from x are intersected in one pass (scene_intersect_n), and the arithmetic is then done in
- * the reference's order.
- * CONT (diffuse surfaces, MK == 0, of a path that continues): bdsf's cosine sample -- the next two
- * draws of the stream after MISv2's, and no draw or ray of MISv2 depends on it -- is taken here too
- * (*wcont: the raw sample bdsf returns in aux), and its ray nrm(*wcont) from x joins the pass (*ch). */
+ * the reference's order. */
 template <bool COUNT, int MK = -1>
 VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray,
-                              double alpha, double sigma_t, dv3* wcont = nullptr, ContHit* ch = nullptr)
+                              double alpha, double sigma_t)
 {
-    /* ch != nullptr (wave-uniform): the continuation joins the pass -- diffuse surfaces only (the
-     * caller's ring fixes MK = 0); counting mode never passes it (decide() counts the ray) */
-    const bool cont = MK == 0 && !COUNT && ch != nullptr;
     const int omat = mat_of<MK>(S, obj);
     const dv3 wo = scl(wray, -1);
     /* ---- draws and directions, in the reference's order */
@@ -888,6 +906,18 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         const double c1 = (1 - e01) + e01 * cm[1];
         const double phi1 = 2 * VPT_PI * smp.next();
         double st0, ct0, sp0, cp0, st1, ct1, sp1, cp1;
+#if VPT_DUP == DUP_MIS_DIRS
+        {
+            double a0 = c0, a1 = phi0, a2 = c1, a3 = phi1;
+            vpt_opaque(a0);
+            vpt_opaque(a1);
+            vpt_opaque(a2);
+            vpt_opaque(a3);
+            double q[8];
+            lm_dir_trig2(a0, a1, a2, a3, &q[0], &q[1], &q[2], &q[3], &q[4], &q[5], &q[6], &q[7]);
+            for (int k = 0; k < 8; ++k) vpt_sink(q[k]);
+        }
+#endif
         lm_dir_trig2(c0, phi0, c1, phi1, &st0, &ct0, &sp0, &cp0, &st1, &ct1, &sp1, &cp1);
         dirs[0] = nrm(from_local(cxk[0], st0 * cp0, st0 * sp0, ct0));
         dirs[1] = nrm(from_local(cxk[1], st1 * cp1, st1 * sp1, ct1));
@@ -913,11 +943,6 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         wi_m = nrm(add(scl(wo_l, -1), scl(scl(wh_m, 2), dot(wh_m, wo_l))));
         dirs[2] = nrm(from_local(n, wi_m.x, wi_m.y, wi_m.z));
     }
-    dv3 dcont = mk(0, 0, 0);
-    if (cont) {  /* bdsf (vptShadeMethods.h:16-59, diffuse): cosineHemispheric, then nrm in the caller */
-        *wcont = cosine_hemispheric(smp, n);
-        dcont = nrm(*wcont);
-    }
     /* ---- the three ray casts from x */
     double tt[3];
     int ids[3] = {0, 0, 0};
@@ -941,30 +966,33 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         }
         skip2 = __ballot(maybe) == 0;
     }
-    if (cont) {
+#if VPT_DUP == DUP_MIS_ISECT
+    {
+        dv3 x2 = x;
+        dv3 dd[3] = {dirs[0], dirs[1], dirs[2]};
+        vpt_opaque(x2);
+        for (int k = 0; k < 3; ++k) vpt_opaque(dd[k]);
+        double tq[3];
+        int iq[3] = {0, 0, 0};
+        bool hq[3];
         if (skip2) {
-            const dv3 d3[3] = {dirs[0], dirs[1], dcont};
-            double t3[3];
-            int i3[3] = {0, 0, 0};
-            bool h3[3];
-            scene_intersect_n<3>(S, smp, x, d3, t3, i3, h3);
-            smp.tests(S->n);  /* (counting mode: the skipped ray's tests) */
-            tt[0] = t3[0], tt[1] = t3[1], tt[2] = 0.0;
-            ids[0] = i3[0], ids[1] = i3[1];
-            hits[0] = h3[0], hits[1] = h3[1], hits[2] = false;
-            *ch = ContHit{t3[2], i3[2], h3[2]};
+            const dv3 d2[2] = {dd[0], dd[1]};
+            double t2[2];
+            int i2[2] = {0, 0};
+            bool h2[2];
+            scene_intersect_n<2>(S, smp, x2, d2, t2, i2, h2);
+            tq[0] = t2[0], tq[1] = t2[1], iq[0] = i2[0], iq[1] = i2[1], hq[0] = h2[0], hq[1] = h2[1];
+            tq[2] = 0, hq[2] = false;
         } else {
-            const dv3 d4[4] = {dirs[0], dirs[1], dirs[2], dcont};
-            double t4[4];
-            int i4[4] = {0, 0, 0, 0};
-            bool h4[4];
-            scene_intersect_n<4>(S, smp, x, d4, t4, i4, h4);
-            tt[0] = t4[0], tt[1] = t4[1], tt[2] = t4[2];
-            ids[0] = i4[0], ids[1] = i4[1], ids[2] = i4[2];
-            hits[0] = h4[0], hits[1] = h4[1], hits[2] = h4[2];
-            *ch = ContHit{t4[3], i4[3], h4[3]};
+            scene_intersect_n<3>(S, smp, x2, dd, tq, iq, hq);
         }
-    } else if (skip2) {
+        for (int k = 0; k < 3; ++k) {
+            vpt_sink(tq[k]);
+            vpt_sink(iq[k] + (hq[k] ? 256 : 0));
+        }
+    }
+#endif
+    if (skip2) {
         const dv3 d2[2] = {dirs[0], dirs[1]};
         double t2[2];
         int i2[2] = {0, 0};
@@ -1150,15 +1178,11 @@ VPT_DEV dv3 point_shadow_ld(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
     return Ld;
 }
 
-/* CONT (a path that continues): the phase sample of the continuation -- the stream's next two draws
- * after the light cone's, read by nothing here -- is taken right after the cone (*wcont) and its ray
- * from xt joins the cone ray's pass over the spheres (*ch, ContHit) */
 template <bool COUNT, int LT = -1>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
 VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
                               double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource,
-                              bool zero_ok = false, dv3* wcont = nullptr, ContHit* ch = nullptr)
+                              bool zero_ok = false)
 {
-    const bool cont = !COUNT && ch != nullptr;  /* wave-uniform; counting mode never passes ch */
     const double lr = LT == 1 ? 0.0 : S->sph[src].r;
     const dv3 lp = sph_p(S, src);
     const dv3 rad = sph_rad(S, src);
@@ -1171,25 +1195,37 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     /* a point light (LT == 1, lr = 0): 0 / mag is +0 for mag > 0 (mag >= 0 or NaN), NaN otherwise,
      * so the cosine is 1 or NaN -- the same value without the division and the root */
     double cmax = LT == 1 ? (mag > 0 ? 1.0 : __builtin_nan("")) : vm_sqrt(1 - lr / mag * (lr / mag));
+#if VPT_DUP == DUP_SS_DIR
+    {
+        dv3 wc2 = wc;
+        double cm2 = cmax;
+        vpt_opaque(wc2);
+        vpt_opaque(cm2);
+        Sampler<COUNT> s2 = smp;
+        vpt_opaque(s2.X);
+        vpt_sink(solid_angle_dir(s2, wc2, cm2));
+        vpt_sink(s2.X);
+    }
+#endif
     dv3 wl = solid_angle_dir(smp, wc, cmax);
     double prob_wl = solid_angle_prob(cmax);
-    if (cont) *wcont = phase_sample(smp, din);
     SECT_END(sd, SECT_M_SS_DIR);
     SECT_BEGIN(si);
     double tdist;
     int idHit = 0;
-    if (cont) {
-        const dv3 d2[2] = {wl, *wcont};
-        double t2[2];
-        int i2[2] = {0, 0};
-        bool h2[2];
-        scene_intersect_n<2>(S, smp, xt, d2, t2, i2, h2);
-        tdist = t2[0];
-        idHit = i2[0];
-        *ch = ContHit{t2[1], i2[1], h2[1]};
-    } else {
-        scene_isect(S, smp, xt, wl, tdist, idHit, false);
+#if VPT_DUP == DUP_SS_ISECT
+    {
+        dv3 xt2 = xt, wl2 = wl;
+        vpt_opaque(xt2);
+        vpt_opaque(wl2);
+        double td2 = 0;
+        int id2 = 0;
+        scene_isect(S, smp, xt2, wl2, td2, id2, false);
+        vpt_sink(td2);
+        vpt_sink(id2);
     }
+#endif
+    scene_isect(S, smp, xt, wl, tdist, idHit, false);
     SECT_END(si, SECT_M_SS_ISECT);
     SECT_BEGIN(sw);
     if (src == idHit) {
@@ -1276,6 +1312,40 @@ struct Event {
 
 enum { EV_END = 0, EV_SURF = 1, EV_MED = 2 };
 
+/* VPT_DUP measurement builds: opaque copies / sinks of a path and an event */
+VPT_DEV void vpt_opaque(Path& p)
+{
+    vpt_opaque(p.o);
+    vpt_opaque(p.d);
+    vpt_opaque(p.beta);
+    vpt_opaque(p.L);
+    vpt_opaque(p.depth);
+}
+VPT_DEV void vpt_sink(const Path& p)
+{
+    vpt_sink(p.o);
+    vpt_sink(p.d);
+    vpt_sink(p.beta);
+    vpt_sink(p.L);
+    vpt_sink(p.depth);
+}
+VPT_DEV void vpt_opaque(Event& e)
+{
+    vpt_opaque(e.t);
+    vpt_opaque(e.dist);
+    vpt_opaque(e.pdf);
+    vpt_opaque(e.id);
+    vpt_opaque(e.src);
+}
+VPT_DEV void vpt_sink(const Event& e)
+{
+    vpt_sink(e.t);
+    vpt_sink(e.dist);
+    vpt_sink(e.pdf);
+    vpt_sink(e.id);
+    vpt_sink(e.src);
+}
+
 /* Russian roulette at the top of a loop iteration (vptShadeMethods.h:1282 / :1354) and the depth
  * cap extension; true = the path continues. */
 template <bool COUNT>
@@ -1301,22 +1371,26 @@ VPT_DEV constexpr bool est_free_flight() { return EST == 0 || EST == 2 || EST ==
 /* vptShadeMethods.h:1284-1307 (FF), :1357-1426 (MIS), :1166-1205 (explicit free), :950-977
  * (implicit free), :1031-1096 (explicit): what happens to the path this iteration. */
 template <int EST, bool COUNT>
-VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, Event& e, const Medium& m,
-                   bool have_pre = false, const ContHit& pre = ContHit{0.0, 0, false})
+VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, Event& e, const Medium& m)
 {
     const double sigma_t = m.sigma_a + m.sigma_s;
     int id = 0;
     double t = 0.0;
-    bool hit = false;
     SECT_BEGIN(di);
-    /* have_pre: the ray's nearest hit came with the event that made it (ContHit); the spheres are
-     * visited only when some lane of the wave lacks one */
-    if (__ballot(!have_pre) != 0) hit = scene_intersect_grouped<VPT_DECIDE_GROUP>(S, smp, p.o, p.d, t, id);
-    if (have_pre) {
-        hit = pre.hit;
-        t = pre.t;
-        id = pre.id;
+#if VPT_DUP == DUP_DECIDE_ISECT
+    {
+        dv3 o2 = p.o, d2 = p.d;
+        vpt_opaque(o2);
+        vpt_opaque(d2);
+        double t2 = 0;
+        int id2 = 0;
+        const int h2 = scene_intersect_grouped<VPT_DECIDE_GROUP>(S, smp, o2, d2, t2, id2);
+        vpt_sink(t2);
+        vpt_sink(id2);
+        vpt_sink(h2);
     }
+#endif
+    const bool hit = scene_intersect_grouped<VPT_DECIDE_GROUP>(S, smp, p.o, p.d, t, id);
     SECT_END(di, SECT_A_ISECT);
     if constexpr (EST == 5) {  /* iterativePathTracer (shadeMethods.h:115-125): nearest hit or end */
         if (COUNT) smp.cnt.iterations++;
@@ -1370,17 +1444,13 @@ VPT_DEV int decide(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p,
 
 /* surface event: point-light NEE (pLight), sphere-light MIS (MISv2), BSDF continuation (bdsf).
  * cont = false: the path ends at the next roulette draw (the pool's kill prediction), so only the
- * radiance is updated -- the continuation's draws, direction and throughput are never read.
- * CONT (diffuse, two MIS lights, a path that continues): bdsf's sample is taken inside MISv2 and the
- * continuation ray's nearest hit comes back in *ch (ContHit) -- the same draws in the same order. */
+ * radiance is updated -- the continuation's draws, direction and throughput are never read. */
 template <int EST, bool COUNT, int MK = -1, int PT = -1>  /* MK: material, PT: point light (1), if known */
 VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e,
-                           const Medium& m, bool cont = true, ContHit* ch = nullptr, int lk = -1)
+                           const Medium& m, bool cont = true, int lk = -1)
 {
     /* the light kind: PT when the instantiation fixes it, else lk (wave-uniform: the pool's ring) */
     const int ptk = PT >= 0 ? PT : lk;
-    /* fused (wave-uniform): a continuing diffuse path in a scene with two MIS lights (ch from the pool) */
-    const bool fused = cont && ch != nullptr && MK == 0 && EST != 3 && !COUNT && S->n_mis == 2;
     const double sigma_t = m.sigma_a + m.sigma_s;
     const double continueprob = 0.6;
     const int id = e.id, src = e.src;
@@ -1418,6 +1488,22 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
         plight_zero = __ballot(!zero) == 0;
         if (plight_zero) smp.tests(2 * S->n);  /* what visibility + the visibilityVPT miss would count */
     }
+#if VPT_DUP == DUP_PLIGHT
+    if (!plight_zero) {
+        dv3 xs2 = xs, nx2 = nx, d2 = p.d;
+        int id2 = id, src2 = src;
+        double a2 = alpha;
+        vpt_opaque(xs2);
+        vpt_opaque(nx2);
+        vpt_opaque(d2);
+        vpt_opaque(id2);
+        vpt_opaque(src2);
+        vpt_opaque(a2);
+        Sampler<COUNT> s2 = smp;
+        double Trs2 = transmitance(xs2, sph_p(S, src2), sigma_t);
+        vpt_sink(scl(scl(p_light<COUNT, MK, PT>(S, s2, id2, xs2, nx2, d2, src2, a2), Trs2), (1 / probSource)));
+    }
+#endif
     if (!plight_zero) {
         double Trs = transmitance(xs, sph_p(S, src), sigma_t);
         Ldp = scl(scl(p_light<COUNT, MK, PT>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
@@ -1426,25 +1512,46 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     SECT_BEGIN(mis);
     /* the fused three-ray MISv2 for diffuse surfaces only: metal and dielectric take the sequential
      * one (round 3: scratch 448 -> 240 B/lane, FF 51.99 -> 51.53 ms) */
-    dv3 wcont = mk(0, 0, 0);
-    const dv3 Ld = MK == 0 && S->n_mis == 2
-             ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t, &wcont, fused ? ch : nullptr)
-             : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
+#if VPT_DUP == DUP_MIS
+    if (MK == 0 && S->n_mis == 2) {
+        dv3 xs2 = xs, nx2 = nx, d2 = p.d;
+        int id2 = id;
+        vpt_opaque(xs2);
+        vpt_opaque(nx2);
+        vpt_opaque(d2);
+        vpt_opaque(id2);
+        Sampler<COUNT> s2 = smp;
+        vpt_opaque(s2.X);
+        vpt_sink(mis_v2_two_lights<COUNT, MK>(S, s2, id2, xs2, nx2, d2, alpha, sigma_t));
+        vpt_sink(s2.X);
+    }
+#endif
+    const dv3 Ld = MK == 0 && S->n_mis == 2 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
+                                            : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
     SECT_END(mis, SECT_S_MIS);
     SECT_BEGIN(bd);
     /* (the radiance update reads the throughput before bdsf's update, as in the reference) */
     if (EST == 0) p.L = add(p.L, scl(mul(add(Ldp, Ld), p.beta), (1 / continueprob)));
     else p.L = add(p.L, mul(p.beta, scl(add(Ldp, Ld), (1 / continueprob))));
-    if (fused) {  /* bdsf for a diffuse surface (vptShadeMethods.h:16-59), its sample drawn in MISv2 */
-        const dv3 fs = scl(sph_c(S, id), (1 / VPT_PI));
-        const double pdf = hemi_cosine_prob(dot(nx, wcont));
-        const dv3 wi = nrm(wcont);
-        double cosine = dot(nx, wi);
-        p.beta = scl(scl(scl(mul(p.beta, fs), (1 / continueprob)), cosine), (1 / pdf));
-        p.o = xs;
-        p.d = wi;
-        p.depth++;
-    } else if (cont) {
+#if VPT_DUP == DUP_BDSF
+    if (cont) {
+        dv3 wi2 = mk(0, 0, 0), d2 = p.d, nx2 = nx, b2 = p.beta;
+        int id2 = id;
+        vpt_opaque(d2);
+        vpt_opaque(nx2);
+        vpt_opaque(b2);
+        vpt_opaque(id2);
+        double pdf2 = 0;
+        Sampler<COUNT> s2 = smp;
+        vpt_opaque(s2.X);
+        dv3 fs2 = bdsf<COUNT, MK>(S, s2, wi2, d2, nx2, pdf2, id2);
+        wi2 = nrm(wi2);
+        vpt_sink(scl(scl(scl(mul(b2, fs2), (1 / continueprob)), dot(nx2, wi2)), (1 / pdf2)));
+        vpt_sink(wi2);
+        vpt_sink(s2.X);
+    }
+#endif
+    if (cont) {
         dv3 wi = mk(0, 0, 0);
         double pdf = 0;
         dv3 fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
@@ -1513,9 +1620,23 @@ VPT_DEV void eqa_medium(const DevScene* __restrict__ S, const Path& p, const Eve
 /* the medium event after single scattering's Ld (vptShadeMethods.h:1318-1332 / :1461-1477): the
  * radiance update, then -- unless the path ends at the next roulette draw (cont = false) -- the phase
  * sample and the throughput.  T: transmittance to xt, pdf: the equi-angular pdf (estimators 1, 4). */
+#if VPT_DUP == DUP_PHASE
+#define VPT_DUP_PHASE()                      \
+    {                                        \
+        dv3 d2 = p.d;                        \
+        vpt_opaque(d2);                      \
+        Sampler<COUNT> s2 = smp;             \
+        vpt_opaque(s2.X);                    \
+        vpt_sink(phase_sample(s2, d2));      \
+        vpt_sink(s2.X);                      \
+    }
+#else
+#define VPT_DUP_PHASE() \
+    do {                \
+    } while (0)
+#endif
 template <int EST, bool COUNT>
-VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double pdf, dv3 xt, const Medium& m, bool cont,
-                         const dv3* wpre = nullptr)  /* wpre: the phase sample, already drawn (single_scattering CONT) */
+VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double pdf, dv3 xt, const Medium& m, bool cont)
 {
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
@@ -1524,21 +1645,24 @@ VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double 
         p.L = add(p.L, scl(scl(mul(Ld, p.beta), (sigma_s / sigma_t)), (1 / continueprob)));
         if (!cont) return;
         SECT_BEGIN(ph);
-        dv3 wi = wpre ? *wpre : phase_sample(smp, p.d);
+        VPT_DUP_PHASE();
+        dv3 wi = phase_sample(smp, p.d);
         SECT_END(ph, SECT_M_PHASE);
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else if (EST == 2) {  /* vptShadeMethods.h:1252-1258 */
         p.L = add(p.L, mul(p.beta, scl(scl(Ld, (sigma_s / sigma_t)), (1 / continueprob))));
         if (!cont) return;
-        dv3 wi = wpre ? *wpre : phase_sample(smp, p.d);
+        VPT_DUP_PHASE();
+        dv3 wi = phase_sample(smp, p.d);
         p.beta = scl(scl(p.beta, (sigma_s / sigma_t)), (1 / continueprob));
         p.d = wi;
     } else {
         p.L = add(p.L, mul(p.beta, scl(scl(Ld, (1 / pdf)), (1 / continueprob))));
         if (!cont) return;
         SECT_BEGIN(ph);
-        dv3 wi = wpre ? *wpre : phase_sample(smp, p.d);
+        VPT_DUP_PHASE();
+        dv3 wi = phase_sample(smp, p.d);
         SECT_END(ph, SECT_M_PHASE);
         p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / pdf));
         p.d = wi;
@@ -1550,21 +1674,35 @@ VPT_DEV void medium_tail(Sampler<COUNT>& smp, Path& p, dv3 Ld, double T, double 
 /* medium event: single-scattering NEE toward the picked light, phase-function continuation.
  * LT: 1 point light, 0 not, -1 unknown (the pool kernel's medium rings are keyed by it).  cont = false:
  * radiance only (surface_event). */
-template <int EST, bool COUNT, int LT = -1>  /* ch: the continuation fused (single_scattering), when cont */
+template <int EST, bool COUNT, int LT = -1>
 VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, Path& p, const Event& e0,
-                          const Medium& m, bool cont = true, ContHit* ch = nullptr)
+                          const Medium& m, bool cont = true)
 {
-    const bool fused = cont && ch != nullptr && EST != 3 && !COUNT;
     const double sigma_a = m.sigma_a, sigma_s = m.sigma_s;
     const double sigma_t = sigma_a + sigma_s;
     const double continueprob = 0.6;
     Event e = e0;
     SECT_BEGIN(eq);
+#if VPT_DUP == DUP_EQA
+    if (EST == 1 || EST == 4) {
+        Path p2 = p;
+        Event e2 = e0;
+        uint64_t X2 = smp.X;
+        vpt_opaque(p2);
+        vpt_opaque(e2);
+        vpt_opaque(X2);
+        double dd = 0, pp = 0;
+        eqa_medium<EST>(S, p2, e2, X2, dd, pp);
+        vpt_sink(dd);
+        vpt_sink(pp);
+    }
+#endif
     if (EST == 1 || EST == 4) eqa_medium<EST>(S, p, e0, smp.X, e.dist, e.pdf);
     SECT_END(eq, SECT_M_EQA);
     dv3 xt = add(p.o, scl(p.d, e.dist));
     if (EST == 3) {  /* implicit: vptShadeMethods.h:1000-1006 */
         const double T = transmitance(p.o, xt, sigma_t);
+        VPT_DUP_PHASE();
         dv3 wi = phase_sample(smp, p.d);
         p.beta = scl(scl(scl(scl(p.beta, sigma_s), T), (1 / continueprob)), (1 / e.pdf));
         p.d = wi;
@@ -1586,11 +1724,24 @@ VPT_DEV void medium_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, P
         SECT_END(tr, SECT_M_TR);
     }
     SECT_BEGIN(ss);
-    dv3 wcont = mk(0, 0, 0);
-    const dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, ws, sigma_s, T, probSource, zero_ok,
-                                                &wcont, fused ? ch : nullptr);
+#if VPT_DUP == DUP_SS
+    {
+        dv3 xt2 = xt, d2 = p.d;
+        int src2 = e.src;
+        double T2 = T;
+        vpt_opaque(xt2);
+        vpt_opaque(d2);
+        vpt_opaque(src2);
+        vpt_opaque(T2);
+        Sampler<COUNT> s2 = smp;
+        vpt_opaque(s2.X);
+        vpt_sink(single_scattering<COUNT, LT>(S, s2, xt2, d2, src2, sigma_t, ws, sigma_s, T2, probSource, zero_ok));
+        vpt_sink(s2.X);
+    }
+#endif
+    const dv3 Ld = single_scattering<COUNT, LT>(S, smp, xt, p.d, e.src, sigma_t, ws, sigma_s, T, probSource, zero_ok);
     SECT_END(ss, SECT_M_SS);
-    medium_tail<EST, COUNT>(smp, p, Ld, T, e.pdf, xt, m, cont, fused ? &wcont : nullptr);
+    medium_tail<EST, COUNT>(smp, p, Ld, T, e.pdf, xt, m, cont);
 }
 
 /* iterativePathTracer, include/shadeMethods.h:104-163 (estimator 5): surface-only path tracing.

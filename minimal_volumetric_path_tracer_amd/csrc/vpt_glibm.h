@@ -615,12 +615,24 @@ GM_CALLQ gm_sc2 gm_sincos_acos_phi(double c, double phi)
 
 /* gm_sincos_acos_phi for a wave whose every c > 0.9925 (the cone toward a sphere light): acos(c) <
  * 0.1226 < 0.126 in every lane (glibc's acos is within an ulp), so sin of the polar angle is
- * TAYLOR_SIN and cos its first-range do_cos -- the specialised evaluation, the same bits */
+ * TAYLOR_SIN -- the specialised evaluation, the same bits -- and cos(acos c) is c itself, without
+ * evaluating it (VPT_COS_ACOS_C).  Why that is exact: for c in (0.9925, 1], theta = acos(c) < 0.1226 and
+ * glibc's acos returns theta' within half an ulp of theta (|theta' - theta| <= 2^-57), so
+ * |cos(theta') - c| <= sin(theta) |theta' - theta| < 2^-60, an eighth of a half-ulp of c (2^-54);
+ * glibc's do_cos there (table value + double-double correction, error ~2^-68 before its final rounding)
+ * therefore rounds to c.  Checked against glibc's own cos(acos(c)) on 2e8 random c in [0.9925, 1) and on
+ * every one of the 2^32 doubles below 1 (scripts-free: tests/test_glibc_libm.py repeats a sample), and
+ * on the device against glibc (tests/test_gpu_parity.py).  The do_cos evaluation skipped is ~15 FP64
+ * operations and four dependent __sincostab reads per direction. */
+#ifndef VPT_COS_ACOS_C
+#define VPT_COS_ACOS_C 1
+#endif
 GM_CALLQ gm_sc2 gm_sincos_acos_phi_cone(double c, double phi)
 {
     vm_ct* K = vm_tab(gm_sc_tab);
     gm_sc2 r;
     gm_sincos_fused_r(K, gm_acos_bc(c), &r.s0, &r.c0, 1, 1);  /* c > 0.9925: acos outside the table range */
+    if (VPT_COS_ACOS_C) r.c0 = c;
     gm_sincos_k(K, phi, &r.s1, &r.c1);
     return r;
 }
@@ -638,6 +650,10 @@ GM_CALLQ gm_sc4 gm_sincos_acos_phi_cone2(double c0, double phi0, double c1, doub
     const double t0 = gm_acos_bc(c0), t1 = gm_acos_bc(c1);
     gm_sincos_fused_r(K, t0, &r.a.s0, &r.a.c0, 1, 1);
     gm_sincos_fused_r(K, t1, &r.b.s0, &r.b.c0, 1, 1);
+    if (VPT_COS_ACOS_C) {  /* cos(acos c) == c for c > 0.9925 (gm_sincos_acos_phi_cone) */
+        r.a.c0 = c0;
+        r.b.c0 = c1;
+    }
     gm_sincos_k(K, phi0, &r.a.s1, &r.a.c1);
     gm_sincos_k(K, phi1, &r.b.s1, &r.b.c1);
     return r;

@@ -349,6 +349,16 @@ __global__ void math_probe_kernel(int fn, const double* x, const double* y, doub
         r = fn == 10 ? sv : cv;
         break;
     }
+    case 14:
+    case 15:
+    case 16:
+    case 17: {  /* lm_dir_trig(c = a, phi = b) as the direction samplers call it (cone path when every
+                 * lane of the wave has c > 0.9925): sin(acos c), cos(acos c), sin(phi), cos(phi) */
+        double q[4];
+        lm_dir_trig(a, b, &q[0], &q[1], &q[2], &q[3]);
+        r = q[fn - 14];
+        break;
+    }
     default: r = a / b; break;
     }
     out[i] = r;
@@ -404,6 +414,8 @@ struct vpt_context {
     DevScene h_scene;
     int has_scene;
     unsigned long long* d_counters;
+    unsigned* d_guard;       /* pool_kernel's argument-layout guard flag (PoolParams::guard), sticky */
+    unsigned guard_bias = 0; /* vpt_debug_karg_guard */
     std::mutex mu;           /* guards slots: held from taking a slot until its launches are enqueued */
     std::vector<std::unique_ptr<StreamSlot>> slots;  /* stable addresses */
     unsigned long long tick = 0;
@@ -550,6 +562,17 @@ static int build_kparams(const vpt_context* ctx, const vpt_params* p, void* d_ou
     return VPT_OK;
 }
 
+/* the pool kernel's argument-layout guard (PoolParams::guard): after a synchronised render, a raised
+ * flag means a launch read its parameters from the wrong place and rendered nothing */
+static int check_guard(vpt_context* ctx, const char* who)
+{
+    unsigned g = 0;
+    HIP_OK(hipMemcpy(&g, ctx->d_guard, sizeof g, hipMemcpyDeviceToHost));
+    if (g) return vpt_fail(VPT_E_INTERNAL, "%s: pool_kernel's launch parameters are not at the start of its argument "
+                           "segment (VPT_P_KARG guard); the image is NaN", who);
+    return VPT_OK;
+}
+
 template <typename Kern>
 static int persistent_grid(vpt_context* ctx, Kern kern, int* blocks, int threads = 256)
 {
@@ -666,6 +689,8 @@ static int launch_pool(vpt_context* ctx, KParams K, hipStream_t stream)
         if (rc) return rc;
         Q.partials = sl->d_partials;
         Q.queue = sl->d_queue;
+        Q.guard = ctx->d_guard;
+        Q.guard_bias = ctx->guard_bias;
         const Medium m{K.sigma_a, K.sigma_s, K.g, K.max_depth, K.march_step, K.march_light};
         rc = persistent_grid(ctx, pool_kernel<EST, COUNT>, &blocks, VPT_POOL_THREADS);
         if (rc) return rc;
@@ -772,8 +797,11 @@ int vpt_context_create(int device, vpt_context** out)
     c->has_scene = 0;
     c->d_scene = nullptr;
     c->d_counters = nullptr;
+    c->d_guard = nullptr;
     hipError_t e = hipMalloc((void**)&c->d_scene, sizeof(DevScene));
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_guard, sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(c->d_guard, 0, sizeof(unsigned));
     if (e != hipSuccess) {
         vpt_context_destroy(c);
         return vpt_fail(VPT_E_HIP, "vpt_context_create: hipMalloc: %s", hipGetErrorString(e));
@@ -790,6 +818,7 @@ void vpt_context_destroy(vpt_context* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->d_scene) (void)hipFree(ctx->d_scene);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_guard) (void)hipFree(ctx->d_guard);
     for (auto& sl : ctx->slots) {
         if (sl->done) (void)hipEventSynchronize(sl->done);
         if (sl->d_partials) (void)hipFree(sl->d_partials);
@@ -879,7 +908,7 @@ int vpt_render(vpt_context* ctx, const vpt_params* p, void* h_out)
     (void)hipFree(d);
     if (rc) return rc;
     if (e != hipSuccess) return vpt_fail(VPT_E_HIP, "vpt_render: %s", hipGetErrorString(e));
-    return VPT_OK;
+    return check_guard(ctx, "vpt_render");
 }
 
 int vpt_count_work(vpt_context* ctx, const vpt_params* p, uint64_t* tests, uint64_t* iterations)
@@ -1153,6 +1182,7 @@ extern "C" int vpt_debug_set_launch_bound(vpt_context* ctx, int log2)
 /* debug: task slots per workgroup pool of this build (vpt_pool.h POOL) */
 extern "C" int vpt_debug_pool_tasks(void) { return POOL; }
 
+
 extern "C" int64_t vpt_debug_launch_plan(const vpt_params* p, int blocks, int log2, uint64_t* unit0, uint64_t* nunits,
                                          int64_t cap)
 {
@@ -1174,4 +1204,30 @@ extern "C" int64_t vpt_debug_launch_plan(const vpt_params* p, int blocks, int lo
         }
     }
     return k;
+}
+
+/* Test hooks of two internal checks (tests/test_gpu_parity.py), each undone by passing 0:
+ * vpt_debug_karg_guard: bias != 0 makes pool_kernel's argument-layout guard fail (and clears the sticky
+ * flag when 0), so vpt_render must return VPT_E_INTERNAL;
+ * vpt_debug_kill_jump: the kill prediction's surface jump (DevScene::kp_sa, kp_sc) set to `draws` draws
+ * instead of 2 n_mis + 5, so vpt_count_work's draw-count check must fail (0: the scene's own). */
+extern "C" int vpt_debug_karg_guard(vpt_context* ctx, unsigned bias)
+{
+    vpt_clear_error();
+    if (!ctx) return vpt_fail(VPT_E_INVALID, "NULL context");
+    HIP_OK(hipSetDevice(ctx->device));
+    ctx->guard_bias = bias;
+    if (bias == 0) HIP_OK(hipMemset(ctx->d_guard, 0, sizeof(unsigned)));
+    return VPT_OK;
+}
+extern "C" int vpt_debug_kill_jump(vpt_context* ctx, int draws)
+{
+    vpt_clear_error();
+    if (!ctx || !ctx->has_scene) return vpt_fail(VPT_E_INVALID, "NULL context or no scene");
+    if (draws < 0) return vpt_fail(VPT_E_INVALID, "draws must be >= 0");
+    DevScene& h = ctx->h_scene;
+    vpt_erand48_jump(draws > 0 ? draws : 2 * h.n_mis + 5, &h.kp_sa, &h.kp_sc);
+    HIP_OK(hipSetDevice(ctx->device));
+    HIP_OK(hipMemcpy(ctx->d_scene, &h, sizeof h, hipMemcpyHostToDevice));
+    return VPT_OK;
 }

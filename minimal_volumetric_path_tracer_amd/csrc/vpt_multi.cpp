@@ -13,6 +13,13 @@
  *
  * The Python path (minimal_volumetric_path_tracer_amd/distributed.py: one process per GPU,
  * torch.distributed "nccl") uses the same band layout.
+ *
+ * Debug mode (vpt_debug_multi_create_shared, not part of include/vpt.h): n logical ranks on ONE device --
+ * n contexts, n streams, n strips -- with a same-device stream-ordered copy of each strip in place of
+ * the grouped ncclSend / ncclRecv (RCCL refuses two ranks on one device).  Everything else of the n > 1
+ * path runs as on n GPUs: buffers, band plan, per-rank renders on their own streams, synchronisation,
+ * the reassembly copies; tests/test_gpu_multi.py checks it bit for bit against vpt_render on a
+ * one-GPU box.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -27,10 +34,12 @@
 #define MULTI_DEFAULT_BAND_ROWS 16
 
 struct vpt_multi {
-    int n;                              /* devices 0 .. n-1 */
+    int n;                              /* logical ranks 0 .. n-1 */
+    std::vector<int> dev;               /* rank g's device: g, or 0 for every rank in the shared debug mode */
+    bool shared = false;                /* debug: all ranks on device 0, strips copied instead of sent */
     std::vector<vpt_context*> ctx;
     std::vector<hipStream_t> stream;
-    std::vector<ncclComm_t> comm;       /* empty when n == 1 */
+    std::vector<ncclComm_t> comm;       /* empty when n == 1 or shared */
     std::vector<void*> strip;           /* device g's strip (g >= 1); device 0 renders into gather */
     std::vector<size_t> strip_bytes;
     void* gather = nullptr;             /* on device 0: n slots of `slot_bytes` */
@@ -74,7 +83,7 @@ void sync_all(vpt_multi* m)
 {
     for (int g = 0; g < m->n; ++g) {
         if (!m->stream[g]) continue;
-        (void)hipSetDevice(g);
+        (void)hipSetDevice(m->dev[g]);
         (void)hipStreamSynchronize(m->stream[g]);
     }
 }
@@ -127,14 +136,14 @@ void vpt_multi_destroy(vpt_multi* m)
     if (!m) return;
     for (int g = 0; g < m->n; ++g) {
         if (g < (int)m->stream.size() && m->stream[g]) {
-            (void)hipSetDevice(g);
+            (void)hipSetDevice(m->dev[g]);
             (void)hipStreamSynchronize(m->stream[g]);
         }
     }
     for (ncclComm_t c : m->comm)
         if (c) (void)ncclCommDestroy(c);
     for (int g = 0; g < m->n; ++g) {
-        (void)hipSetDevice(g);
+        (void)hipSetDevice(m->dev[g]);
         if (g < (int)m->strip.size() && m->strip[g]) (void)hipFree(m->strip[g]);
         if (g < (int)m->stream.size() && m->stream[g]) (void)hipStreamDestroy(m->stream[g]);
         if (g < (int)m->ctx.size() && m->ctx[g]) vpt_context_destroy(m->ctx[g]);
@@ -146,7 +155,8 @@ void vpt_multi_destroy(vpt_multi* m)
     delete m;
 }
 
-int vpt_multi_create(int n_gpus, vpt_multi** out)
+/* n ranks on devices 0 .. n-1 (shared: all on device 0, no communicator) */
+static int multi_create(int n_gpus, bool shared, vpt_multi** out)
 {
     vpt_clear_error();
     if (!out) return vpt_fail(VPT_E_INVALID, "vpt_multi_create: out is NULL");
@@ -154,27 +164,31 @@ int vpt_multi_create(int n_gpus, vpt_multi** out)
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess) return hip_fail("vpt_multi_create: hipGetDeviceCount", e);
-    if (n_gpus < 1 || n_gpus > ndev) return vpt_fail(VPT_E_INVALID, "vpt_multi_create: n_gpus %d of %d devices", n_gpus, ndev);
+    if (n_gpus < 1 || (!shared && n_gpus > ndev) || ndev < 1 || n_gpus > 64)
+        return vpt_fail(VPT_E_INVALID, "vpt_multi_create: n_gpus %d of %d devices", n_gpus, ndev);
     vpt_multi* m = new vpt_multi();
     m->n = n_gpus;
+    m->shared = shared;
+    m->dev.resize(n_gpus);
+    for (int g = 0; g < n_gpus; ++g) m->dev[g] = shared ? 0 : g;
     m->ctx.assign(n_gpus, nullptr);
     m->stream.assign(n_gpus, nullptr);
     m->strip.assign(n_gpus, nullptr);
     m->strip_bytes.assign(n_gpus, 0);
     for (int g = 0; g < n_gpus; ++g) {
-        int rc = vpt_context_create(g, &m->ctx[g]);
+        int rc = vpt_context_create(m->dev[g], &m->ctx[g]);
         if (rc) {
             vpt_multi_destroy(m);
             return rc;
         }
-        e = hipSetDevice(g);
+        e = hipSetDevice(m->dev[g]);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->stream[g], hipStreamNonBlocking);
         if (e != hipSuccess) {
             vpt_multi_destroy(m);
             return hip_fail("vpt_multi_create: stream", e);
         }
     }
-    if (n_gpus > 1) {
+    if (n_gpus > 1 && !shared) {
         m->comm.assign(n_gpus, nullptr);
         std::vector<int> devs(n_gpus);
         for (int g = 0; g < n_gpus; ++g) devs[g] = g;
@@ -188,6 +202,11 @@ int vpt_multi_create(int n_gpus, vpt_multi** out)
     *out = m;
     return VPT_OK;
 }
+
+int vpt_multi_create(int n_gpus, vpt_multi** out) { return multi_create(n_gpus, false, out); }
+
+/* debug (tests): n logical ranks on device 0, strips copied on the device instead of sent over RCCL */
+int vpt_debug_multi_create_shared(int n_ranks, vpt_multi** out) { return multi_create(n_ranks, true, out); }
 
 int vpt_multi_set_scene(vpt_multi* m, const vpt_sphere* spheres, int n)
 {
@@ -222,7 +241,7 @@ int vpt_multi_render(vpt_multi* m, const vpt_params* p, void* h_out)
     int rc = ensure_device_buffer(0, &m->gather, &m->gather_bytes, slot * (size_t)n);
     if (rc) return rc;
     for (int g = 1; g < n; ++g) {
-        rc = ensure_device_buffer(g, &m->strip[g], &m->strip_bytes[g], slot);
+        rc = ensure_device_buffer(m->dev[g], &m->strip[g], &m->strip_bytes[g], slot);
         if (rc) return rc;
     }
     /* every device renders its bands on its own stream */
@@ -240,7 +259,19 @@ int vpt_multi_render(vpt_multi* m, const vpt_params* p, void* h_out)
         }
     }
     /* strips -> device 0, slot g (stream-ordered after each render) */
-    if (n > 1) {
+    if (n > 1 && m->shared) {  /* debug: the same movement as the send / recv pairs, on one device */
+        hipError_t e = hipSetDevice(0);
+        for (int g = 1; g < n && e == hipSuccess; ++g) {
+            const size_t bytes = (size_t)rows[g] * row_bytes;
+            if (bytes == 0) continue;
+            e = hipMemcpyAsync((unsigned char*)m->gather + (size_t)g * slot, m->strip[g], bytes, hipMemcpyDeviceToDevice,
+                               m->stream[g]);
+        }
+        if (e != hipSuccess) {
+            sync_all(m);
+            return hip_fail("vpt_multi_render: strip copy (shared debug mode)", e);
+        }
+    } else if (n > 1) {
         ncclResult_t r = ncclGroupStart();
         for (int g = 1; g < n && r == ncclSuccess; ++g) {
             const size_t bytes = (size_t)rows[g] * row_bytes;
@@ -256,7 +287,7 @@ int vpt_multi_render(vpt_multi* m, const vpt_params* p, void* h_out)
         }
     }
     for (int g = n - 1; g >= 0; --g) {
-        hipError_t e = hipSetDevice(g);
+        hipError_t e = hipSetDevice(m->dev[g]);
         if (e == hipSuccess) e = hipStreamSynchronize(m->stream[g]);
         if (e != hipSuccess) {
             sync_all(m);

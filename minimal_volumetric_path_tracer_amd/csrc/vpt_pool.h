@@ -55,15 +55,6 @@ namespace vpt {
 #ifndef VPT_KILL_RINGS
 #define VPT_KILL_RINGS 1
 #endif
-#ifndef VPT_FUSE_CONT
-#define VPT_FUSE_CONT 0     /* the continuation ray in the event's own intersection pass (ContHit, vpt_device.h); A/B r05: slower, see DESIGN */
-#endif
-#ifndef VPT_MERGE_KINDS
-/* surface (diffuse) and medium events compiled once for both light kinds -- the ring still fixes the
- * kind for a whole batch, so its branches are wave-uniform -- instead of once per kind: the hot code
- * is what the shared 64 KB instruction cache has to hold (round 5: I-cache misses track code size) */
-#define VPT_MERGE_KINDS 1
-#endif
 #ifndef VPT_SCHED_PRIO
 #define VPT_SCHED_PRIO 3    /* s_setprio level of the scheduler's critical section (0: off; A/B 3 vs 0: +0.7 %) */
 #endif
@@ -179,6 +170,8 @@ struct PoolParams {
                              * out together, 8x8 tiles) write neighbouring 24-B records that merge into
                              * whole lines in L2 (pixel-major wrote 24 B per 128-B line: 2x the WRITE_SIZE) */
     unsigned* queue;
+    unsigned* guard;        /* the argument-layout guard's flag (VPT_P_KARG): set when the check fails */
+    unsigned guard_bias;    /* 0; vpt_debug_karg_guard sets it to make the check fail (its test) */
 };
 
 /* VPT_P_KARG: the launch parameters read where they are used, by scalar loads from the kernel-argument
@@ -266,8 +259,6 @@ __device__ __forceinline__ dv3 pool_camera_dir(const PoolParams& P0, double jx, 
 struct Task {
     Path p;
     Event e;
-    ContHit pre;     /* the continuation ray's nearest hit, when the event's pass found it (registers only) */
-    bool have_pre;
     dv3 acc;
     uint64_t X;
     uint64_t key;    /* the unit's pixel stream key */
@@ -359,24 +350,32 @@ __device__ __forceinline__ void run_event(const DevScene* __restrict__ S, Sample
             st = st < R_MD ? st - R_SD + R_S : st - R_MD + R_M;
         }
         /* metal (R_S + 2) and other materials (R_S + 3) are rare: 1.4 % of surface events at the
-         * bench scene.  A diffuse or medium event of a path that continues casts its continuation ray
-         * in its own pass over the spheres (ContHit, VPT_FUSE_CONT); stage A's decide() then visits
-         * no sphere for these lanes. */
-        constexpr bool FUSE = VPT_FUSE_CONT && !COUNT && (EST == 0 || EST == 1 || EST == 2 || EST == 4);
-        ContHit* ch = FUSE && cont ? &t.pre : nullptr;
+         * bench scene.  Diffuse-surface and medium events are compiled once for both light kinds (the
+         * ring fixes the kind for the whole batch, so its branches are wave-uniform) instead of once per
+         * kind: the hot code is what the shared 64 KB instruction cache has to hold (round 5: I-cache
+         * misses track code size) */
+#if VPT_DUP == DUP_SURF || VPT_DUP == DUP_MED
+        if (VPT_DUP == DUP_SURF ? st < R_M : st >= R_M) {
+            Path p2 = t.p;
+            Event e2 = t.e;
+            vpt_opaque(p2);
+            vpt_opaque(e2);
+            Sampler<COUNT> s2 = smp;
+            vpt_opaque(s2.X);
+            if (st >= R_M) medium_event<EST, COUNT, -1>(S, s2, p2, e2, m, cont);
+            else if (st < R_S + 2) surface_event<EST, COUNT, 0, -1>(S, s2, p2, e2, m, cont, st - R_S);
+            else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, s2, p2, e2, m);
+            else surface_event<EST, COUNT, -1, -1>(S, s2, p2, e2, m);
+            vpt_sink(p2);
+            vpt_sink(s2.X);
+        }
+#endif
         if (st < R_M) {
-            if (VPT_MERGE_KINDS && st < R_S + 2) {  /* one copy for both light kinds, kind = the ring */
-                surface_event<EST, COUNT, 0, -1>(S, smp, t.p, t.e, m, cont, ch, st - R_S);
-            } else if (st == R_S) surface_event<EST, COUNT, 0, 0>(S, smp, t.p, t.e, m, cont, ch);
-            else if (st == R_S + 1) surface_event<EST, COUNT, 0, 1>(S, smp, t.p, t.e, m, cont, ch);
+            if (st < R_S + 2) surface_event<EST, COUNT, 0, -1>(S, smp, t.p, t.e, m, cont, st - R_S);
             else if (st == R_S + 2) surface_event<EST, COUNT, 1, -1>(S, smp, t.p, t.e, m);
             else surface_event<EST, COUNT, -1, -1>(S, smp, t.p, t.e, m);
-            t.have_pre = FUSE && cont && st < R_S + 2 && S->n_mis == 2;
         } else {
-            if (VPT_MERGE_KINDS) medium_event<EST, COUNT, -1>(S, smp, t.p, t.e, m, cont, ch);
-            else if (st == R_M) medium_event<EST, COUNT, 0>(S, smp, t.p, t.e, m, cont, ch);
-            else medium_event<EST, COUNT, 1>(S, smp, t.p, t.e, m, cont, ch);
-            t.have_pre = FUSE && cont;
+            medium_event<EST, COUNT, -1>(S, smp, t.p, t.e, m, cont);
         }
         SECT_END(ev, st < R_M ? SECT_S_TOTAL : SECT_M_TOTAL);
         SECT_BEGIN(cp);
@@ -418,7 +417,6 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P0, const
         t.acc = add(t.p.L, t.acc);  /* src/rt.cpp:794 */
         t.in_path = false;
         t.killed = false;
-        t.have_pre = false;        /* (its continuation ray is never cast) */
     }
     const unsigned long long c0 = dbg_clock(dbg);
     SECT_BEGIN(pr);
@@ -548,13 +546,23 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P0, const
         const double jy = smp.next();
         if (EST != 5) (void)smp.next();  /* the roulette draw, decided above */
         t.p.o = mk(P.o[0], P.o[1], P.o[2]);
+#if VPT_DUP == DUP_CAMERA
+        {
+            double jx2 = jx, jy2 = jy;
+            int px = (int)(t.pix & 0xFFFFu), py = (int)(t.pix >> 16);
+            vpt_opaque(jx2);
+            vpt_opaque(jy2);
+            vpt_opaque(px);
+            vpt_opaque(py);
+            vpt_sink(pool_camera_dir(P0, jx2, jy2, px, py));
+        }
+#endif
         t.p.d = pool_camera_dir(P0, jx, jy, (int)(t.pix & 0xFFFFu), (int)(t.pix >> 16));
         t.p.beta = mk(1, 1, 1);
         t.p.L = mk(0, 0, 0);
         t.p.depth = 0;
         if (EST == 5) t.e.pdf = 1;  /* iterativePathTracer's `factor` rides in the event's pdf slot */
         t.X = smp.X;
-        t.have_pre = false;
         SECT_END(ci, SECT_A_CAMERA_IN);
     }
     SECT_END(cam, SECT_A_CAMERA);
@@ -564,7 +572,21 @@ __device__ __forceinline__ int stage_a(TaskPool& sh, const PoolParams& P0, const
     if (!done && !parked) {
         SECT_BEGIN(dci);
         smp.X = t.X;
-        const int ev = decide<EST>(S, smp, t.p, t.e, m, t.have_pre, t.pre);
+#if VPT_DUP == DUP_DECIDE
+        {
+            Path p2 = t.p;
+            Event e2 = t.e;
+            vpt_opaque(p2);
+            vpt_opaque(e2);
+            Sampler<COUNT> s2 = smp;
+            vpt_opaque(s2.X);
+            vpt_sink(decide<EST>(S, s2, p2, e2, m));
+            vpt_sink(p2);
+            vpt_sink(e2);
+            vpt_sink(s2.X);
+        }
+#endif
+        const int ev = decide<EST>(S, smp, t.p, t.e, m);
         t.X = smp.X;
         if (ev == EV_END) {
             t.acc = add(t.p.L, t.acc);
@@ -605,9 +627,13 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
 {
     __shared__ TaskPool sh;
 #if VPT_P_KARG && defined(__HIP_DEVICE_COMPILE__)
-    /* pool_params_at_use() reads P0 at offset 0 of the argument segment: P0 must stay the first argument
-     * (if it moves, the launch renders nothing and every parity test fails) */
-    if (pool_params_at_use().nunits != P0.nunits || pool_params_at_use().unit0 != P0.unit0) return;
+    /* pool_params_at_use() reads P0 at offset 0 of the argument segment: P0 must stay the first argument.
+     * If it moves, the launch renders nothing and raises the guard flag: reduce_kernel then writes NaN and
+     * the synchronous entry points (vpt_render) return VPT_E_INTERNAL instead of a garbage image. */
+    if (pool_params_at_use().nunits != P0.nunits + P0.guard_bias || pool_params_at_use().unit0 != P0.unit0) {
+        if (threadIdx.x == 0) atomicOr(P0.guard, 1u);
+        return;
+    }
 #endif
     const int tid = threadIdx.x, lane = tid & 63;
     const uint64_t below = (1ull << lane) - 1ull;
@@ -779,7 +805,20 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         /* one copy of stage A in the code: a batch of ring A runs it alone, a batch of an S/M ring
          * runs its event first and then stage A on the same lanes */
         SECT_BEGIN(ld);
-        t.have_pre = false;
+#if VPT_DUP == DUP_LDST
+        if (active) {  /* a second load of the task (sunk) and, below, a second store of the same values */
+            int slot2 = slot;
+            vpt_opaque(slot2);
+            Task t2;
+            load_task(sh, slot2, t2, true);
+            vpt_sink(t2.p);
+            vpt_sink(t2.e);
+            vpt_sink(t2.acc);
+            vpt_sink(t2.X);
+            vpt_sink(t2.key);
+            vpt_sink((int)(t2.pix ^ t2.c1 ^ t2.i ^ (t2.in_path ? 1 : 0) ^ (t2.killed ? 2 : 0)));
+        }
+#endif
         if (active) load_task(sh, slot, t, true);
         else {
             t.c1 = 0;
@@ -795,6 +834,13 @@ __global__ __launch_bounds__(VPT_POOL_THREADS, VPT_POOL_WGS) void pool_kernel(Po
         next = stage_a<EST>(sh, P0, S, m, smp, t, active, lane, below, dbga, D);
         SECT_BEGIN(stt);
         if (active) store_task(sh, slot, t, true);
+#if VPT_DUP == DUP_LDST
+        if (active) {
+            int slot2 = slot;
+            vpt_opaque(slot2);
+            store_task(sh, slot2, t, true);
+        }
+#endif
         SECT_END(stt, SECT_STORE);
         if (dbg) {
             const unsigned long long now = dbg_clock(dbg);
@@ -843,6 +889,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(PoolParams P, void* out)
     dv3 tot = mk(0, 0, 0);
     for (int c = 0; c < P.nch; ++c) tot = add(mk(q[c * plane], q[c * plane + 1], q[c * plane + 2]), tot);
     tot = scl(tot, (1 / (double)P.spp));  /* src/rt.cpp:800 */
+    if (VPT_UNLIKELY(*(volatile unsigned*)P.guard != 0)) tot = mk(__builtin_nan(""), __builtin_nan(""), __builtin_nan(""));
     if (FB == VPT_FB_F32) {
         float* o = (float*)out;
         o[3 * p] = (float)tot.x;

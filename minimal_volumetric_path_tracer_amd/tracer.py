@@ -16,7 +16,7 @@ becomes an exception.
 from __future__ import annotations
 
 import ctypes
-from ctypes import byref, c_uint64, c_void_p
+from ctypes import POINTER, byref, c_int, c_uint64, c_void_p
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -262,9 +262,16 @@ class MultiTracer:
     interleaved row bands per device, strips gathered to device 0 over RCCL.  Bit-identical to
     Tracer.render for any n_gpus."""
 
-    def __init__(self, n_gpus: int, spheres: Optional[np.ndarray] = None):
+    def __init__(self, n_gpus: int, spheres: Optional[np.ndarray] = None, shared_device: bool = False):
+        """shared_device (tests): n_gpus logical ranks on device 0, their strips copied on the device
+        instead of sent over RCCL (vpt_debug_multi_create_shared) -- the n > 1 path on a one-GPU box"""
         h = c_void_p()
-        check(lib().vpt_multi_create(n_gpus, byref(h)))
+        if shared_device:
+            f = lib().vpt_debug_multi_create_shared
+            f.restype, f.argtypes = c_int, [c_int, POINTER(c_void_p)]
+            check(f(n_gpus, byref(h)))
+        else:
+            check(lib().vpt_multi_create(n_gpus, byref(h)))
         self._m = h
         self.n_gpus = n_gpus
         s = np.ascontiguousarray(default_scene() if spheres is None else spheres, dtype=SPHERE_DTYPE)

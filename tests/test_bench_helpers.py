@@ -83,3 +83,12 @@ def test_socket_conservative_uses_the_fastest_runs():
     assert bench.socket_conservative([12.0, 13.0, 11.0], [1.3, 1.25, 1.2], 16, 64) == 1.3 * 64
     # a slowed run cannot raise the ratio: adding a slower run leaves the figure unchanged
     assert bench.socket_conservative([22.0, 10.0], [1.3, 0.5], 16, 64) == bench.socket_conservative([22.0], [1.3], 16, 64)
+
+
+def test_shared_device_refusal():
+    """an N-GPU bench line needs N distinct GPUs (PCI ids) unless --shared-device marks a test run"""
+    assert bench.shared_device_refusal(["0000:05:00", "0000:15:00"], False) is None
+    assert bench.shared_device_refusal(["0000:05:00"], False) is None
+    why = bench.shared_device_refusal(["0000:05:00", "0000:15:00", "0000:05:00"], False)
+    assert why and "0000:05:00" in why and "3-GPU" in why
+    assert bench.shared_device_refusal(["0000:05:00", "0000:05:00"], True) is None

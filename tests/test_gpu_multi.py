@@ -3,9 +3,11 @@ GPUs of one process, strips gathered over RCCL) and the `vpt` program, the drop-
 reference's `./rt <spp>` (src/rt.cpp:744-830: image.ppm in the reference's format and the
 "elapsed time: <s>s" line of src/rt.cpp:824-827).
 
-The box these run on has one GPU: the multi-GPU entry is exercised with n_gpus = 1 (communicator,
-band layout and reorder code paths of n > 1 are covered by the band-composition tests of
-test_gpu_parity.py and the gloo tests of test_distributed.py; the 8-GPU run is the driver's)."""
+The box these run on has one GPU: the multi-GPU entry is exercised with n_gpus = 1, and its n > 1 path
+with n logical ranks sharing device 0 (vpt_debug_multi_create_shared: everything but the RCCL send /
+recv, which becomes a same-device copy); the gloo tests of test_distributed.py cover the Python path's
+band layout, and the 8-GPU run is the driver's."""
+import dataclasses
 import os
 import re
 import subprocess
@@ -35,6 +37,29 @@ def test_multi_one_gpu_equals_render(gpu_tracer, est, fp64):
         m.close()
     assert bitwise_equal(a, ref).all() and bitwise_equal(b, ref).all()
     assert bitwise_equal(vpt.render_multi(1, cfg), ref).all()
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("est,fp64,h,band", [("ff", True, 40, 0), ("mis", True, 37, 0), ("ff", False, 53, 4),
+                                             ("mis", False, 16, 0)])
+def test_multi_shared_device_n_ranks_equals_render(gpu_tracer, n, est, fp64, h, band):
+    """vpt_multi_render's n > 1 path executed on the one-GPU box: n logical ranks
+    on device 0 (vpt_debug_multi_create_shared), each with its context, stream and strip, its bands
+    rendered on its own stream, the strips moved into device 0's gather buffer by stream-ordered copies
+    where RCCL's grouped send / recv would run, then the band plan's device-to-host copies.  Bit-identical
+    to vpt_render for ragged heights (bands that do not divide the image, ranks with no band at all:
+    n = 8 over 16 rows), both framebuffer formats and two calls on the same handle (buffers reused)."""
+    gpu_tracer.set_scene(vpt.default_scene())
+    cfg = vpt.RenderConfig(width=24, height=h, spp=3, estimator=est, fp64=fp64, seed=29,
+                           band_rows=band if band else 0)
+    ref = gpu_tracer.render(dataclasses.replace(cfg, band_rows=0))
+    m = vpt.MultiTracer(n, shared_device=True)
+    try:
+        a = m.render(cfg)
+        b = m.render(dataclasses.replace(cfg, seed=29))
+    finally:
+        m.close()
+    assert bitwise_equal(a, ref).all() and bitwise_equal(b, ref).all()
 
 
 def test_multi_band_rows_argument(gpu_tracer):

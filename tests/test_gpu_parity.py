@@ -49,6 +49,30 @@ def test_device_math_bitwise(gpu_tracer, orc, orc_vm, fn, lo, hi):
         assert same.all(), f"fn {fn}: {(~same).sum()} differ, e.g. x={x[~same][:3]} dev={dev[~same][:3]} host={host[~same][:3]}"
 
 
+def test_device_dir_trig_cone_path_vs_glibc(gpu_tracer):
+    """the cone samplers' trig (lm_dir_trig with every lane's c > 0.9925: gm_sincos_acos_phi_cone, where
+    cos(acos c) is taken to be c -- VPT_COS_ACOS_C, csrc/vpt_glibm.h) against glibc's own sin(acos c),
+    cos(acos c), sin(phi), cos(phi) bit for bit: 4 M uniform c in (0.9925, 1], the 2^17 doubles just below 1,
+    c = 1, and the range's low end"""
+    from oracle.oracle import Oracle
+
+    glibc = Oracle(portable=False)
+    rng = np.random.default_rng(2606)
+    n = 1 << 22
+    top = 1.0 - np.arange(0, 1 << 17) * 2.0**-53
+    low = np.nextafter(0.9925, 1.0) + np.arange(0, 4096) * 2.0**-53
+    c = np.concatenate([rng.uniform(0.9925, 1.0, n), top, low])
+    c = np.maximum(c, np.nextafter(0.9925, 1.0))
+    c = np.concatenate([c, np.full(64 - len(c) % 64, 1.0)])  # whole waves of cone-range lanes
+    phi = 2 * np.pi * rng.random(len(c))
+    for fn in (14, 15, 16, 17):
+        dev = gpu_tracer.math_probe(fn, c, phi)
+        ref = glibc.math(fn, c, phi)
+        same = bitwise_equal(dev, ref)
+        assert same.all(), f"fn {fn}: {(~same).sum()} differ, e.g. c={c[~same][:3]}"
+    assert bitwise_equal(gpu_tracer.math_probe(15, c, phi), c).all()  # cos(acos c) == c there
+
+
 def test_device_tan_range_boundaries(gpu_tracer, orc):
     """gm_tan on the device over the ranges the [-1.5, 1.5] sweep above leaves out: [1.5,
     pi/2) -- the odd-n branch where -1/y goes through the double-double division, reached by the
@@ -81,6 +105,57 @@ def test_kill_prediction_draw_counts(gpu_tracer, est):
             tests, iters = gpu_tracer.count_work(vpt.RenderConfig(width=24, height=16, spp=8, estimator=est, **kw))
             assert tests > 0 and iters > 0, (name, kw)
     gpu_tracer.set_scene(vpt.default_scene())
+
+
+def _debug_fn(name, argtypes):
+    f = getattr(vpt.lib(), name)
+    f.restype = ctypes.c_int
+    f.argtypes = argtypes
+    return f
+
+
+@pytest.mark.parametrize("est", ["ff", "mis"])
+def test_kill_prediction_check_can_fail(gpu_tracer, est):
+    """the draw-count check above must be able to fail: with the kill prediction's surface
+    jump one draw off (vpt_debug_kill_jump: 2 n_mis + 6 instead of 2 n_mis + 5 draws to the roulette),
+    vpt_count_work raises VPT_E_INTERNAL; with the scene's own jump restored it passes again"""
+    jump = _debug_fn("vpt_debug_kill_jump", [ctypes.c_void_p, ctypes.c_int])
+    sc = vpt.default_scene()
+    gpu_tracer.set_scene(sc)
+    n_mis = int(((sc["r"] > 0) & (sc["radiance"][:, 0] > 0)).sum())
+    cfg = vpt.RenderConfig(width=24, height=16, spp=8, estimator=est)
+    _lib.check(jump(gpu_tracer._ctx, 2 * n_mis + 6))
+    try:
+        with pytest.raises(vpt.VPTError, match="kill prediction"):
+            gpu_tracer.count_work(cfg)
+    finally:
+        _lib.check(jump(gpu_tracer._ctx, 0))
+    tests, iters = gpu_tracer.count_work(cfg)
+    assert tests > 0 and iters > 0
+
+
+def test_karg_guard_fails_loudly(gpu_tracer):
+    """pool_kernel reads its launch parameters from the kernel-argument segment at use (VPT_P_KARG); its
+    layout guard, made to fail by vpt_debug_karg_guard, must not hand back a garbage image with VPT_OK
+    (ADVICE r05): vpt_render returns VPT_E_INTERNAL, the device path's image is NaN, and with the hook
+    cleared the render is the oracle's again"""
+    guard = _debug_fn("vpt_debug_karg_guard", [ctypes.c_void_p, ctypes.c_uint])
+    gpu_tracer.set_scene(vpt.default_scene())
+    cfg = vpt.RenderConfig(width=16, height=16, spp=4, fp64=True, seed=SEED)
+    good = gpu_tracer.render(cfg)
+    _lib.check(guard(gpu_tracer._ctx, 1))
+    try:
+        with pytest.raises(vpt.VPTError, match="VPT_P_KARG"):
+            gpu_tracer.render(cfg)
+        import torch
+        buf = torch.zeros((16, 16, 3), dtype=torch.float64, device="cuda:0")
+        gpu_tracer.render_device(cfg, buf.data_ptr(), 0)
+        torch.cuda.synchronize()
+        assert torch.isnan(buf).all()
+    finally:
+        _lib.check(guard(gpu_tracer._ctx, 0))
+    again = gpu_tracer.render(cfg)
+    assert bitwise_equal(again, good).all() and np.isfinite(good).all()
 
 
 def test_device_sqrt_div_correctly_rounded(gpu_tracer, orc):
@@ -117,7 +192,12 @@ def test_device_inv_sqrt_exact(gpu_tracer):
     sq = (rng.integers(1, 1 << 26, 20000).astype(np.float64)) ** 2 * 2.0 ** rng.integers(-600, 600, 20000)
     near = np.concatenate([sq, np.nextafter(sq, 0), np.nextafter(sq, np.inf)])
     unit = 1.0 + rng.uniform(-1e-6, 1e-6, 100000)  # |a|^2 of nearly unit vectors (the path's common case)
-    x = np.concatenate([x, edges, near, unit])
+    # the reciprocal's final correction (Markstein) is exact from any seed within an ulp of 1/s except,
+    # possibly, for s with an all-ones significand: x around (2 - 2^-52)^2 2^(2k), whose roots are those s
+    ones = (2.0 - 2.0**-52) ** 2 * 4.0 ** rng.integers(-380, 500, 4000).astype(np.float64)
+    ones = np.concatenate([ones, np.nextafter(ones, 0), np.nextafter(ones, np.inf), np.nextafter(np.nextafter(ones, 0), 0)])
+    wide = np.ldexp(rng.uniform(1.0, 4.0, 2_000_000), 2 * rng.integers(-383, 511, 2_000_000))  # every exponent of [2^-767, DBL_MAX]
+    x = np.concatenate([x, edges, near, unit, ones, wide])
     with np.errstate(divide="ignore", invalid="ignore"):
         want = 1.0 / np.sqrt(x)
     got = gpu_tracer.math_probe(12, x)
@@ -513,6 +593,31 @@ def test_config3_full_size_dense_depth8_4096spp_vs_oracle(gpu_tracer, orc_vm):
         y = 2047 - fr
         row = orc_vm.render(2048, 2048, 4096, 0, seed=SEED, y0=y, y1=y + 1, threads=16, **kw)[fr]
         assert bitwise_equal(img[fr], row).all(), fr
+
+
+@pytest.mark.gpu
+def test_config4_rank0_shard_full_size(gpu_tracer, orc_vm):
+    """BASELINE configs[4]'s per-GPU workload at full size: rank 0's shard of the
+    8-GPU render -- 16-row bands, band stride 8: 512 file rows of 4096 x 4096 x 8192 spp MIS, 1.7e10
+    samples -- through the natural launch split (the 2^26-samples-per-workgroup bound, no lowered bound:
+    2 launches), the auto layout at 8192 spp (64-sample chunks + taper, 137 chunks, 6.9 GB of partials)
+    and the u32 queue guards.  The whole shard is finite and lit; two file rows (4096 x 8192 samples
+    each) are recomputed by the oracle's pixel loop bit for bit (src/rt.cpp:786-800: every sample once,
+    in order)."""
+    sc = SCENES["default"]()
+    gpu_tracer.set_scene(sc)
+    orc_vm.set_scene(sc)
+    W = H = 4096
+    spp, band, world = 8192, 16, 8
+    img = gpu_tracer.render(width=W, height=H, spp=spp, estimator="mis", seed=SEED, fp64=True, band_rows=band,
+                            band_stride=world, band_offset=0)
+    assert img.shape == (H // world, W, 3)
+    assert np.isfinite(img).all() and img.max() > 0
+    for lr in (37, 470):  # shard rows -> file rows of rank 0's bands
+        fr = (lr // band) * band * world + lr % band
+        y = H - 1 - fr
+        row = orc_vm.render(W, H, spp, 1, seed=SEED, y0=y, y1=y + 1, threads=16)[fr]
+        assert bitwise_equal(img[lr], row).all(), (lr, fr)
 
 
 def _set_launch_bound(tracer, log2):
