@@ -212,16 +212,50 @@ VPT_DEV double sphere_tact(double b, double det)
     return tact;
 }
 
-/* the nearest-contact update of intersect() (include/pathTracingUtilities.h:17-30); branches, not
- * selects (A/B round 2: 56.8 vs 57.7 ms with selects at FF 1024^2 x 256) */
+/* the nearest-contact update of intersect() (include/pathTracingUtilities.h:17-30) as selects
+ * (VPT_TAKE_SEL): two compares and three selects instead of two nested branches -- their exec-mask
+ * bookkeeping is ~6 scalar instructions per sphere test, in the wave's one instruction stream.  Round 2
+ * measured selects slower (56.8 vs 57.7 ms FF); on the round-6 kernel they are faster (A/B ab_r06b: FF
+ * 40.39 -> 39.88 ms, MIS + HG 181.1 -> 177.9 ms). */
+#ifndef VPT_TAKE_SEL
+#define VPT_TAKE_SEL 1
+#endif
 VPT_DEV void sphere_take(double tact, int i, double& tmin, int& id, int& contact)
 {
+    if (VPT_TAKE_SEL) {
+        const bool c = tact > 0.0001;
+        const bool take = c && tact < tmin;
+        tmin = take ? tact : tmin;
+        id = take ? i : id;
+        contact = c ? 1 : contact;
+        return;
+    }
     if (tact > 0.0001) {
         contact = 1;
         if (tact < tmin) {
             tmin = tact;
             id = i;
         }
+    }
+}
+
+/* one sphere's contact and the nearest-contact update together (VPT_TAKE_IN): the update inside the
+ * det >= 0 branch, so a wave whose every lane misses the sphere (det < 0: no contact, tact = 0 would
+ * be taken by no lane) skips it as well as the root -- the same tmin, id and contact per lane */
+#ifndef VPT_TAKE_IN
+#define VPT_TAKE_IN 1
+#endif
+VPT_DEV void sphere_test(double b, double det, int i, double& tmin, int& id, int& contact)
+{
+    if (!VPT_TAKE_IN) {
+        sphere_take(sphere_tact(b, det), i, tmin, id, contact);
+        return;
+    }
+    if (det >= 0) {
+        const double sq = ISECT_SQRT(det);
+        const double t2 = -b + sq;
+        const double t1 = -b - sq;
+        sphere_take(t1 < 0.0001 ? t2 : t1, i, tmin, id, contact);
     }
 }
 
@@ -246,7 +280,7 @@ VPT_DEV int scene_intersect(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
         double b = ocx * d.x + ocy * d.y + ocz * d.z;
         double cc = ocx * ocx + ocy * ocy + ocz * ocz;
         double det = b * b - cc + g.r2;
-        sphere_take(sphere_tact(b, det), i, tmin, id, contact);
+        sphere_test(b, det, i, tmin, id, contact);
     }
     smp.tests(skip3 ? S->n_non3 : n);
     if (contact) {
@@ -281,7 +315,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         }
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            sphere_take(sphere_tact(b[k], det[k]), i + k, tmin, id, contact);
+            sphere_test(b[k], det[k], i + k, tmin, id, contact);
         }
     }
     for (; i < n; ++i) {
@@ -290,7 +324,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         const double b = ocx * d.x + ocy * d.y + ocz * d.z;
         const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
         const double det = b * b - cc + g.r2;
-        sphere_take(sphere_tact(b, det), i, tmin, id, contact);
+        sphere_test(b, det, i, tmin, id, contact);
     }
     smp.tests(n);
     if (contact) {
@@ -322,13 +356,13 @@ VPT_DEV int scene_intersect_grouped_oc(const DevScene* __restrict__ S, Sampler<C
             det[k] = b[k] * b[k] - cc + S->geo[i + k].r2;
         }
 #pragma unroll
-        for (int k = 0; k < G; ++k) sphere_take(sphere_tact(b[k], det[k]), i + k, tmin, id, contact);
+        for (int k = 0; k < G; ++k) sphere_test(b[k], det[k], i + k, tmin, id, contact);
     }
     for (; i < n; ++i) {
         const double ocx = oc[i][0], ocy = oc[i][1], ocz = oc[i][2], cc = oc[i][3];
         const double b = ocx * d.x + ocy * d.y + ocz * d.z;
         const double det = b * b - cc + S->geo[i].r2;
-        sphere_take(sphere_tact(b, det), i, tmin, id, contact);
+        sphere_test(b, det, i, tmin, id, contact);
     }
     smp.tests(n);
     if (contact) {
@@ -391,7 +425,20 @@ VPT_DEV int visibility(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 
 /* coordinateSystem, include/mathUtilities.h:10-19 */
 VPT_DEV void coord_system(dv3 n, dv3& s, dv3& t)
 {
-    if (vm_fabs(n.x) > vm_fabs(n.y)) {
+#ifndef VPT_FRAME_SEL
+#define VPT_FRAME_SEL 1
+#endif
+    if (VPT_FRAME_SEL) {
+        /* the reference's two branches as one evaluation: with u = n.x or n.y by the branch condition, both
+         * compute invLen = 1 / sqrt(u u + n.z n.z) and t from n.z invLen and -(u invLen) (negation is
+         * exact) -- the same operations per lane, but a wave whose lanes take both branches (surface
+         * normals of different walls, cone axes) pays one root and one division instead of two each */
+        const bool bx = vm_fabs(n.x) > vm_fabs(n.y);
+        const double u = bx ? n.x : n.y;
+        const double invLen = 1.0 / vm_sqrt(u * u + n.z * n.z);
+        const double a = n.z * invLen, c = -u * invLen;
+        t = mk(bx ? a : 0.0, bx ? 0.0 : a, c);
+    } else if (vm_fabs(n.x) > vm_fabs(n.y)) {
         double invLen = 1.0 / vm_sqrt(n.x * n.x + n.z * n.z);
         t = mk(n.z * invLen, 0.0, -n.x * invLen);
     } else {
@@ -485,8 +532,38 @@ VPT_DEV dv3 solid_angle_dir(Sampler<COUNT>& smp, dv3 wc, double cmax)
 
 /* solidAngleProb, include/samplingFunctions.h:85-87 */
 VPT_DEV double solid_angle_prob(double cmax) { return 1 / (2 * VPT_PI * (1 - cmax)); }
-/* hemiCosineProb, include/samplingFunctions.h:92-94 */
-VPT_DEV double hemi_cosine_prob(double c) { return c * 1 / VPT_PI; }
+
+/* VPT_DIV_SHARE: divisions by one divisor share its reciprocal (vm_rcp, vpt_math.h) -- the same bits as
+ * the compiler's division for operands it would not rescale, which a wave-uniform range test checks
+ * (else the plain divisions run for the whole wave) */
+#ifndef VPT_DIV_SHARE
+#define VPT_DIV_SHARE 1
+#endif
+/* RN(1/pi), the reciprocal the compiler's division sequence forms for the divisor pi (v_rcp_f64 + two
+ * Newton steps; equal on the device, tests/test_gpu_parity.py::test_device_shared_reciprocal_division) */
+#define VPT_INV_PI_RCP 0x1.45f306dc9c883p-2
+/* hemiCosineProb, include/samplingFunctions.h:92-94: c * 1 / pi, (c * 1) == c */
+VPT_DEV double hemi_cosine_prob(double c)
+{
+    if (VPT_DIV_SHARE && __ballot(!vm_rcp_ok(c)) == 0) {
+        const vm_rcp R = {VPT_PI, VPT_INV_PI_RCP};
+        return vm_div_by(c, R);
+    }
+    return c * 1 / VPT_PI;
+}
+/* 1 / d and r / d -- r a sphere radius (>= 0; +0 for a point light gives +0 as the division does) --
+ * with one reciprocal, when every lane's d and r are in range */
+VPT_DEV void inv_and_ratio(double d, double r, double& inv, double& q)
+{
+    if (VPT_DIV_SHARE && __ballot(!(vm_rcp_ok(d) && (vm_as_u64(r) == 0 || vm_rcp_ok(r)))) == 0) {
+        const vm_rcp R = vm_rcp_of(d);
+        inv = vm_div_by(1.0, R);
+        q = vm_div_by(r, R);
+    } else {
+        inv = 1 / d;
+        q = r / d;
+    }
+}
 
 /* cosineHemispheric, include/samplingFunctions.h:47-62 */
 template <bool COUNT>
@@ -701,9 +778,11 @@ VPT_DEV dv3 light_sample_sa(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
 {
     dv3 cx = sub(sph_p(S, light), x);
     double normcx = vm_sqrt(dot(cx, cx));
-    cx = scl(cx, (1 / normcx));
     double lr = S->sph[light].r;
-    double cmax = vm_sqrt(1 - (lr / normcx) * (lr / normcx));
+    double inv, q;
+    inv_and_ratio(normcx, lr, inv, q);  /* 1 / normcx, lr / normcx */
+    cx = scl(cx, inv);
+    double cmax = vm_sqrt(1 - q * q);
     cmax_out = cmax;
     dv3 wolocal = scl(wray, -1);
     dv3 wi = solid_angle_dir(smp, cx, cmax);
@@ -848,7 +927,7 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
             for (int k = 0; k < N; ++k) {
                 const double b = ocx * d[k].x + ocy * d[k].y + ocz * d[k].z;
                 const double det = b * b - cc + g.r2;
-                sphere_take(sphere_tact(b, det), i + j, tmin[k], id[k], contact[k]);
+                sphere_test(b, det, i + j, tmin[k], id[k], contact[k]);
             }
         }
     }
@@ -860,7 +939,7 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
         for (int k = 0; k < N; ++k) {
             const double b = ocx * d[k].x + ocy * d[k].y + ocz * d[k].z;
             const double det = b * b - cc + g.r2;
-            sphere_take(sphere_tact(b, det), i, tmin[k], id[k], contact[k]);
+            sphere_test(b, det, i, tmin[k], id[k], contact[k]);
         }
     }
     smp.tests(N * n);
@@ -893,9 +972,11 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         lt[k] = S->mis_light[k];
         dv3 cx = sub(sph_p(S, lt[k]), x);
         const double normcx = vm_sqrt(dot(cx, cx));
-        cx = scl(cx, (1 / normcx));
         const double lr = S->sph[lt[k]].r;
-        cm[k] = vm_sqrt(1 - (lr / normcx) * (lr / normcx));
+        double inv, q;
+        inv_and_ratio(normcx, lr, inv, q);  /* 1 / normcx, lr / normcx */
+        cx = scl(cx, inv);
+        cm[k] = vm_sqrt(1 - q * q);
         cxk[k] = cx;
     }
     if (omat != 2) {  /* both cone samples' draws (e0, phi per light, samplingFunctions.h:65-82), then their trig together */
@@ -1191,10 +1272,18 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     SECT_BEGIN(sd);
     dv3 wc = sub(lp, xt);
     double mag = vm_sqrt(dot(wc, wc));
-    wc = scl(wc, (1 / mag));
     /* a point light (LT == 1, lr = 0): 0 / mag is +0 for mag > 0 (mag >= 0 or NaN), NaN otherwise,
      * so the cosine is 1 or NaN -- the same value without the division and the root */
-    double cmax = LT == 1 ? (mag > 0 ? 1.0 : __builtin_nan("")) : vm_sqrt(1 - lr / mag * (lr / mag));
+    double cmax;
+    if (LT == 1) {
+        wc = scl(wc, (1 / mag));
+        cmax = mag > 0 ? 1.0 : __builtin_nan("");
+    } else {
+        double inv, q;
+        inv_and_ratio(mag, lr, inv, q);  /* 1 / mag, lr / mag */
+        wc = scl(wc, inv);
+        cmax = vm_sqrt(1 - q * q);
+    }
 #if VPT_DUP == DUP_SS_DIR
     {
         dv3 wc2 = wc;

@@ -338,6 +338,33 @@ VM_QUAL double gm_acos_bc(double x)
     return res;
 }
 
+/* gm_acos_bc for x in (0.9925, 1] only -- the cone samplers' cosines (every lane of the wave, checked by
+ * the caller): glibc's range B (0.96875 <= x < 1: 2 asin(sqrt((1 - x)/2))) and x == 1 (+0), the same
+ * operations as gm_acos_bc's B lanes without range C's evaluation and the selects between them
+ * (VPT_ACOS_CONE) */
+VM_QUAL double gm_acos_cone(double x)
+{
+    vm_ct* K = vm_tab(gm_acos_tab);
+    const double z = (1.0 - x) * 0.5;
+    const uint64_t zb = vm_as_u64(z);
+    const double two = vm_as_f64((uint64_t)(511 - (int)(zb >> 53) + 1023) << 52);  /* powtwo[] */
+    double t = GM_INROOT[(zb >> 46) & 0x7f] * two;
+    const double r = gm_fnma(t * t, z, 1.0);
+    double q;
+    VM_HORNER_T(q, K + GA_RT3, 4, r);
+    t = q * t;
+    const double c = z * t;
+    const double h = gm_fnma(t * 0.5, c, 1.5);
+    const double t27 = VM_T(K, GA_T27);
+    const double y = gm_fnma(t27, c, gm_fma(c, t27, c));
+    const double cc = gm_fnma(y, y, z) / gm_fma(h, c, y);
+    double p;
+    VM_HORNER_T(p, K + GA_F6, 6, z);
+    const double pr = (p * z) * (y + cc);
+    const double s = (cc + pr) + y;
+    return x == 1.0 ? 0.0 : s + s;
+}
+
 /* ------------------------------------------------------------------ exp / log (e_exp.c, e_log.c)
  * glibc 2.35's exp and log (the table-driven ones of sysdeps/ieee754/dbl-64, N = 128), FMA build.
  * The common paths are restated here as straight-line code reading the library's own tables (the
@@ -382,7 +409,7 @@ VM_QUAL double gm_exp(double x)
     const double tmp = gm_fma(r2 * r2, p45, gm_fma(p23, r2, r + tail));
     const double scale = vm_as_f64(sbits);
     double v = gm_fma(scale, tmp, scale);
-    if (GM_UNLIKELY(abstop - 0x3c9u >= 0x3fu)) v = gl_exp(x);
+    VM_RARE_FIX(abstop - 0x3c9u >= 0x3fu, v, gl_exp(x));
     return v;
 }
 
@@ -430,7 +457,7 @@ VM_QUAL double gm_log(double x)
     q = gm_fma(q, r2, gm_fma(r, VM_T(K, GL_A0), VM_T(K, GL_A1)));
     const double v2 = gm_fma(r * r2, q, lo) + hi;
     double v = ix + 0xc012000000000000ull <= 0x308ffffffffffull ? v1 : v2;
-    if (GM_UNLIKELY(top - 0x0010u >= 0x7ff0u - 0x0010u)) v = gl_log(x);
+    VM_RARE_FIX(top - 0x0010u >= 0x7ff0u - 0x0010u, v, gl_log(x));
     return v;
 }
 
@@ -497,7 +524,7 @@ VM_QUAL double gm_atan2(double y, double x)
     const double tm500 = VM_T(K, GT_TM500), t500 = VM_T(K, GT_T500);
     const int rare = !(x > 0.0) || !(ay > 0.0) || !(x < __builtin_inf()) || !(ay < __builtin_inf()) ||
                      de < -0x38fffff || ax < tm500 || ay < tm500 || ax > t500 || ay > t500;
-    if (GM_UNLIKELY(rare)) r = gl_atan2(y, x);
+    VM_RARE_FIX(rare, r, gl_atan2(y, x));
     return r;
 }
 
@@ -573,7 +600,7 @@ VM_QUAL double gm_tan(double x)
     const double rTab = todd ? (gi - qt) * -sg : (qt + fi) * sg;
     const double small = VM_T(K, GN_SMALL);
     double res = ax <= VM_T(K, GN_TINY) ? x : ax <= small ? rP : !inR ? rTab : u <= small ? rPoly : rTab;
-    if (GM_UNLIKELY(!(ax <= VM_T(K, GN_BIG)))) res = gl_tan(x);
+    VM_RARE_FIX(!(ax <= VM_T(K, GN_BIG)), res, gl_tan(x));
     return res;
 }
 
@@ -627,11 +654,14 @@ GM_CALLQ gm_sc2 gm_sincos_acos_phi(double c, double phi)
 #ifndef VPT_COS_ACOS_C
 #define VPT_COS_ACOS_C 1
 #endif
+#ifndef VPT_ACOS_CONE
+#define VPT_ACOS_CONE 1
+#endif
 GM_CALLQ gm_sc2 gm_sincos_acos_phi_cone(double c, double phi)
 {
     vm_ct* K = vm_tab(gm_sc_tab);
     gm_sc2 r;
-    gm_sincos_fused_r(K, gm_acos_bc(c), &r.s0, &r.c0, 1, 1);  /* c > 0.9925: acos outside the table range */
+    gm_sincos_fused_r(K, VPT_ACOS_CONE ? gm_acos_cone(c) : gm_acos_bc(c), &r.s0, &r.c0, 1, 1);  /* c > 0.9925: range B */
     if (VPT_COS_ACOS_C) r.c0 = c;
     gm_sincos_k(K, phi, &r.s1, &r.c1);
     return r;
@@ -647,7 +677,7 @@ GM_CALLQ gm_sc4 gm_sincos_acos_phi_cone2(double c0, double phi0, double c1, doub
 {
     vm_ct* K = vm_tab(gm_sc_tab);
     gm_sc4 r;
-    const double t0 = gm_acos_bc(c0), t1 = gm_acos_bc(c1);
+    const double t0 = VPT_ACOS_CONE ? gm_acos_cone(c0) : gm_acos_bc(c0), t1 = VPT_ACOS_CONE ? gm_acos_cone(c1) : gm_acos_bc(c1);
     gm_sincos_fused_r(K, t0, &r.a.s0, &r.a.c0, 1, 1);
     gm_sincos_fused_r(K, t1, &r.b.s0, &r.b.c0, 1, 1);
     if (VPT_COS_ACOS_C) {  /* cos(acos c) == c for c > 0.9925 (gm_sincos_acos_phi_cone) */

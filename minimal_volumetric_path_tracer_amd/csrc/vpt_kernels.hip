@@ -359,6 +359,19 @@ __global__ void math_probe_kernel(int fn, const double* x, const double* y, doub
         r = q[fn - 14];
         break;
     }
+    case 18: {  /* a / b through one shared reciprocal of b (VPT_DIV_SHARE), unconditionally */
+        double bb = b;
+        __asm__ volatile("" : "+v"(bb));
+        r = vm_div_by(a, vm_rcp_of(bb));
+        break;
+    }
+    case 19: r = hemi_cosine_prob(a); break;  /* a * 1 / pi */
+    case 20: {                                /* 1 / a and b / a, their bits xor'ed (inv_and_ratio) */
+        double inv, q;
+        inv_and_ratio(a, b, inv, q);
+        r = __longlong_as_double(__double_as_longlong(inv) ^ __double_as_longlong(q));
+        break;
+    }
     default: r = a / b; break;
     }
     out[i] = r;

@@ -73,6 +73,33 @@ def test_device_dir_trig_cone_path_vs_glibc(gpu_tracer):
     assert bitwise_equal(gpu_tracer.math_probe(15, c, phi), c).all()  # cos(acos c) == c there
 
 
+def test_device_shared_reciprocal_division(gpu_tracer):
+    """VPT_DIV_SHARE (csrc/vpt_math.h vm_rcp, csrc/vpt_device.h): the last three operations of the
+    compiler's division on a reciprocal formed once per divisor give the division's bits for operands in
+    [2^-300, 2^300); hemiCosineProb's c / pi on the constant RN(1/pi), and the 1 / d, r / d pairs of the
+    cone samplers, equal the divisions everywhere (their range tests send the rest to the plain division)"""
+    rng = np.random.default_rng(2608)
+    n = 1 << 21
+    a = np.ldexp(rng.uniform(1, 2, n), rng.integers(-300, 299, n)) * rng.choice([-1.0, 1.0], n)
+    b = np.ldexp(rng.uniform(1, 2, n), rng.integers(-300, 299, n)) * rng.choice([-1.0, 1.0], n)
+    b[: n // 4] = rng.uniform(0.5, 400, n // 4)  # the path's divisors: distances, 2 pi (1 - c), ...
+    a[: n // 8] = 1.0
+    assert bitwise_equal(gpu_tracer.math_probe(18, a, b), a / b).all()
+    assert bitwise_equal(gpu_tracer.math_probe(18, a, np.full(n, np.pi)), a / np.pi).all()
+    edge = np.array([0.0, -0.0, 5e-324, -5e-324, 1e-310, 2.0**-300, np.nextafter(2.0**-300, 0), 2.0**300,
+                     np.nextafter(2.0**300, 0), 1e300, np.inf, -np.inf, np.nan, 1.0, -1.0])
+    c = np.concatenate([rng.uniform(-1, 1, n), edge, np.tile(edge, 64)])  # whole waves of edge values too
+    with np.errstate(all="ignore"):
+        assert bitwise_equal(gpu_tracer.math_probe(19, c), c * 1 / np.pi).all()
+    d = np.concatenate([rng.uniform(1e-3, 500, n), edge, np.tile(edge, 64)])
+    r = rng.choice([0.0, 2.0, 16.5, 1e5, -0.0], len(d))
+    r[-len(edge):] = edge[::-1]
+    with np.errstate(all="ignore"):
+        want = (1 / d).view(np.uint64) ^ (r / d).view(np.uint64)
+    got = gpu_tracer.math_probe(20, d, r).view(np.uint64)
+    assert np.array_equal(got, want), f"{(got != want).sum()} differ"
+
+
 def test_device_tan_range_boundaries(gpu_tracer, orc):
     """gm_tan on the device over the ranges the [-1.5, 1.5] sweep above leaves out: [1.5,
     pi/2) -- the odd-n branch where -1/y goes through the double-double division, reached by the
@@ -192,8 +219,7 @@ def test_device_inv_sqrt_exact(gpu_tracer):
     sq = (rng.integers(1, 1 << 26, 20000).astype(np.float64)) ** 2 * 2.0 ** rng.integers(-600, 600, 20000)
     near = np.concatenate([sq, np.nextafter(sq, 0), np.nextafter(sq, np.inf)])
     unit = 1.0 + rng.uniform(-1e-6, 1e-6, 100000)  # |a|^2 of nearly unit vectors (the path's common case)
-    # the reciprocal's final correction (Markstein) is exact from any seed within an ulp of 1/s except,
-    # possibly, for s with an all-ones significand: x around (2 - 2^-52)^2 2^(2k), whose roots are those s
+    # roots s with an all-ones significand (the reciprocal's exceptional case): x around (2 - 2^-52)^2 2^(2k)
     ones = (2.0 - 2.0**-52) ** 2 * 4.0 ** rng.integers(-380, 500, 4000).astype(np.float64)
     ones = np.concatenate([ones, np.nextafter(ones, 0), np.nextafter(ones, np.inf), np.nextafter(np.nextafter(ones, 0), 0)])
     wide = np.ldexp(rng.uniform(1.0, 4.0, 2_000_000), 2 * rng.integers(-383, 511, 2_000_000))  # every exponent of [2^-767, DBL_MAX]
