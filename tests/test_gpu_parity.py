@@ -100,6 +100,28 @@ def test_device_shared_reciprocal_division(gpu_tracer):
     assert np.array_equal(got, want), f"{(got != want).sum()} differ"
 
 
+def test_device_atan2_wide_and_range_bounds(gpu_tracer, orc):
+    """gm_atan2 on the device (its two divisions by max(|y|, x) on one reciprocal, VPT_DIV_SHARE; operands
+    outside [2^-300, 2^300] to the translated library) against glibc over every exponent of both operands
+    and around the 2^-300 / 2^300 bounds, bit for bit"""
+    from oracle.oracle import Oracle
+
+    glibc = Oracle(portable=False)
+    rng = np.random.default_rng(2609)
+    n = 1 << 20
+    x = np.ldexp(rng.uniform(1, 2, n), rng.integers(-1000, 1000, n))
+    y = np.ldexp(rng.uniform(1, 2, n), rng.integers(-1000, 1000, n)) * rng.choice([-1.0, 1.0], n)
+    b = np.array([2.0**-300, np.nextafter(2.0**-300, 0), np.nextafter(2.0**-300, 1), 2.0**300,
+                  np.nextafter(2.0**300, 0), np.nextafter(2.0**300, np.inf), 1.0, 3.0, 1e-10, 1e10])
+    bx, by = np.meshgrid(b, np.concatenate([b, -b]))
+    x = np.concatenate([x, bx.ravel(), rng.uniform(0, 300, n)])
+    y = np.concatenate([y, by.ravel(), rng.uniform(-400, 400, n)])
+    dev = gpu_tracer.math_probe(8, y, x)
+    ref = glibc.math(8, y, x)
+    same = bitwise_equal(dev, ref)
+    assert same.all(), f"{(~same).sum()} differ, e.g. y={y[~same][:3]} x={x[~same][:3]}"
+
+
 def test_device_tan_range_boundaries(gpu_tracer, orc):
     """gm_tan on the device over the ranges the [-1.5, 1.5] sweep above leaves out: [1.5,
     pi/2) -- the odd-n branch where -1/y goes through the double-double division, reached by the

@@ -1,6 +1,7 @@
 """Every compile-time arm the release build does not take still compiles: the
-kept structural knob (VPT_KILL_RINGS=0, the pool without kill-predicting rings) and the debug builds
-(section timers, scheduler statistics and timelines, the round-1 wave kernel behind VPT_DEBUG_ENV).
+kept structural knob (VPT_KILL_RINGS=0, the pool without kill-predicting rings), the forms the round-6
+changes replaced, and the debug / measurement builds (section timers, scheduler statistics and
+timelines, the round-1 wave kernel behind VPT_DEBUG_ENV, a VPT_DUP build).
 A device-side syntax and template-instantiation check of csrc/vpt_kernels.hip for gfx950 -- seconds,
 no GPU; the A/B builds themselves go through scripts/build_variant.sh."""
 import os
@@ -21,6 +22,11 @@ ARMS = {
     "pool_timeline": ["-DVPT_POOL_DEBUG=2"],
     "debug_env": ["-DVPT_DEBUG_ENV=1"],
     "params_in_sgprs": ["-DVPT_P_KARG=0"],  # launch parameters held for the whole kernel (pre-round-5 form)
+    # the round-6 changes off (the forms they replaced, for A/B): branchy sphere-test update outside the
+    # det >= 0 branch, branchy frames, exec-masked rare paths, plain divisions, general cone acos/cos
+    "round6_off": ["-DVPT_TAKE_SEL=0", "-DVPT_TAKE_IN=0", "-DVPT_FRAME_SEL=0", "-DVPT_RARE_BALLOT=0",
+                   "-DVPT_DIV_SHARE=0", "-DVPT_ACOS_CONE=0", "-DVPT_COS_ACOS_C=0"],
+    "dup_sections": ["-DVPT_DUP=3"],  # a VPT_DUP measurement build (scripts/dup_pmc.sh)
 }
 
 
