@@ -220,14 +220,17 @@ VPT_DEV double sphere_tact(double b, double det)
 #ifndef VPT_TAKE_SEL
 #define VPT_TAKE_SEL 1
 #endif
-VPT_DEV void sphere_take(double tact, int i, double& tmin, int& id, int& contact)
+/* (the contact flag as a bool is not cheaper: across the det >= 0 branch the compiler keeps it in a VGPR
+ * and rebuilds the lane mask from it at every test -- 4 instructions instead of 1) */
+typedef int contact_t;
+VPT_DEV void sphere_take(double tact, int i, double& tmin, int& id, contact_t& contact)
 {
     if (VPT_TAKE_SEL) {
         const bool c = tact > 0.0001;
         const bool take = c && tact < tmin;
         tmin = take ? tact : tmin;
         id = take ? i : id;
-        contact = c ? 1 : contact;
+        contact = c ? (contact_t)1 : contact;
         return;
     }
     if (tact > 0.0001) {
@@ -245,7 +248,7 @@ VPT_DEV void sphere_take(double tact, int i, double& tmin, int& id, int& contact
 #ifndef VPT_TAKE_IN
 #define VPT_TAKE_IN 1
 #endif
-VPT_DEV void sphere_test(double b, double det, int i, double& tmin, int& id, int& contact)
+VPT_DEV void sphere_test(double b, double det, int i, double& tmin, int& id, contact_t& contact)
 {
     if (!VPT_TAKE_IN) {
         sphere_take(sphere_tact(b, det), i, tmin, id, contact);
@@ -268,7 +271,7 @@ VPT_DEV int scene_intersect(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
                             int& id, bool skip3)
 {
     double tmin = VPT_DBL_MAX;
-    int contact = 0;
+    contact_t contact = 0;
     const int n = S->n;
     /* unrolled so that consecutive sphere tests (independent dependency chains until the tmin
      * update, which stays in index order) overlap: +2% on the pool kernel (A/B, scripts/ab.sh) */
@@ -300,7 +303,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
 {
     static_assert(G >= 1, "spheres are taken G >= 1 at a time");
     double tmin = VPT_DBL_MAX;
-    int contact = 0;
+    contact_t contact = 0;
     const int n = S->n;
     int i = 0;
     for (; i + G <= n; i += G) {
@@ -344,7 +347,7 @@ VPT_DEV int scene_intersect_grouped_oc(const DevScene* __restrict__ S, Sampler<C
 {
     static_assert(G >= 1, "spheres are taken G >= 1 at a time");
     double tmin = VPT_DBL_MAX;
-    int contact = 0;
+    contact_t contact = 0;
     const int n = S->n;
     int i = 0;
     for (; i + G <= n; i += G) {
@@ -422,6 +425,23 @@ VPT_DEV int visibility(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 
     return (t > distance || t == 0);
 }
 
+/* visibility() given |light - x| and nrm(light - x), formed once by a caller that needs them as well
+ * (p_light_nee): the same operations */
+template <bool COUNT>
+VPT_DEV int visibility_pre(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 light, double distance, dv3 wl,
+                           bool skip3, double light_r, bool light_is3)
+{
+    if (light_r > 0.0001 && !(skip3 && light_is3) && !(distance < light_r)) {
+        smp.tests(skip3 ? S->n_non3 : S->n);
+        return 0;
+    }
+    const dv3 lx = scl(wl, -1);
+    int id = 0;
+    double t;
+    scene_isect(S, smp, light, lx, t, id, skip3);
+    return (t > distance || t == 0);
+}
+
 /* coordinateSystem, include/mathUtilities.h:10-19 */
 VPT_DEV void coord_system(dv3 n, dv3& s, dv3& t)
 {
@@ -463,6 +483,30 @@ VPT_DEV dv3 from_local(dv3 n, double x1, double y1, double z1)
     return add(add(scl(s, x1), scl(t, y1)), scl(n, z1));
 }
 
+/* The coordinateSystem frame of a normal formed once and shared by an event's to_local / from_local
+ * calls (VPT_FRAME_CSE).  The compiler does not merge repeated coord_system(n) calls: the square root's
+ * wave-uniform rare-argument branch makes each evaluation its own control flow, so every call was a
+ * root, a division and a cross product again (a diffuse surface event formed the frame of its normal
+ * six times).  Same operations, same bits. */
+#ifndef VPT_FRAME_CSE
+#define VPT_FRAME_CSE 1
+#endif
+struct Frame {
+    dv3 s, t, n;
+};
+VPT_DEV Frame make_frame(dv3 n)
+{
+    Frame F;
+    F.n = n;
+    coord_system(n, F.s, F.t);
+    return F;
+}
+VPT_DEV dv3 to_local(const Frame& F, dv3 w) { return mk(dot(F.s, w), dot(F.t, w), dot(F.n, w)); }
+VPT_DEV dv3 from_local(const Frame& F, double x1, double y1, double z1)
+{
+    return add(add(scl(F.s, x1), scl(F.t, y1)), scl(F.n, z1));
+}
+
 /* transmitance, include/volumetricBasicFunctions.h:14-21 */
 VPT_DEV double transmitance(dv3 a, dv3 b, double sigma_t)
 {
@@ -499,7 +543,8 @@ VPT_DEV double multiple_t(const DevScene* __restrict__ S, Sampler<COUNT>& smp, d
 /* ------------------------------------------------------------------ sampling */
 /* direction at polar angle theta = acos(c) and azimuth phi around n: the reference computes
  * sin(acos c), cos(acos c), sin(phi), cos(phi) with libm (lm_dir_trig, bit for bit) */
-VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
+template <class FL>
+VPT_DEV dv3 dir_from_cos_fl(dv3 n, double c, double phi, FL fl)
 {
     double st, ct, sp, cp;
     if (__ballot(c != 1.0) == 0) {
@@ -517,7 +562,15 @@ VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
     } else {
         lm_dir_trig(c, phi, &st, &ct, &sp, &cp);
     }
-    return nrm(from_local(n, st * cp, st * sp, ct));
+    return nrm(fl(st * cp, st * sp, ct));
+}
+VPT_DEV dv3 dir_from_cos(dv3 n, double c, double phi)
+{
+    return dir_from_cos_fl(n, c, phi, [&](double a, double b, double d) { return from_local(n, a, b, d); });
+}
+VPT_DEV dv3 dir_from_cos(const Frame& F, double c, double phi)
+{
+    return dir_from_cos_fl(F.n, c, phi, [&](double a, double b, double d) { return from_local(F, a, b, d); });
 }
 
 /* solidAngle(wc, costheta_max), include/samplingFunctions.h:65-82 */
@@ -572,6 +625,13 @@ VPT_DEV dv3 cosine_hemispheric(Sampler<COUNT>& smp, dv3 n)
     double c = vm_sqrt(1 - smp.next());  /* theta = acos(c) */
     double phi = 2 * VPT_PI * smp.next();
     return dir_from_cos(n, c, phi);
+}
+template <bool COUNT>
+VPT_DEV dv3 cosine_hemispheric(Sampler<COUNT>& smp, const Frame& F)
+{
+    double c = vm_sqrt(1 - smp.next());
+    double phi = 2 * VPT_PI * smp.next();
+    return dir_from_cos(F, c, phi);
 }
 
 /* isotropicPhaseSample, include/vptSamplingFunctions.h:34-47 (g == 0); Henyey-Greenstein
@@ -904,7 +964,7 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
                                double (&t)[N], int (&id)[N], bool (&hit)[N])
 {
     double tmin[N];
-    int contact[N];
+    contact_t contact[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         tmin[k] = VPT_DBL_MAX;
@@ -956,16 +1016,25 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
  * / microfacet), so the draws and directions are taken first in the reference's order, the three
  * rays from x are intersected in one pass (scene_intersect_n), and the arithmetic is then done in
  * the reference's order. */
+/* Fn: the frame of n (make_frame), shared with the caller's pLight and bdsf (held through the three ray
+ * casts: forming it again after them was slower, A/B ab_r06h 38.21 / 171.2 vs 37.91 / 171.0 ms).  VPT_MIS_REUSE: the
+ * transmittance's distance is the light setup's |c - x| (transmitance() forms the same root of the same
+ * dot product), the BSDF sample's hemiCosineProb is formed once for its two uses, and cosinethetaMax of
+ * a light the BSDF ray hit is the setup's cone cosine of that light (the same operations on the same
+ * operands) when every lane's hit is one of the two lights. */
+#ifndef VPT_MIS_REUSE
+#define VPT_MIS_REUSE 1
+#endif
 template <bool COUNT, int MK = -1>
 VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray,
-                              double alpha, double sigma_t)
+                              double alpha, double sigma_t, const Frame& Fn)
 {
     const int omat = mat_of<MK>(S, obj);
     const dv3 wo = scl(wray, -1);
     /* ---- draws and directions, in the reference's order */
     int lt[2];
     dv3 dirs[3];
-    double cm[2], xtra[2] = {0, 0};
+    double cm[2], xtra[2] = {0, 0}, nd[2];
     dv3 cxk[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -978,6 +1047,7 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         cx = scl(cx, inv);
         cm[k] = vm_sqrt(1 - q * q);
         cxk[k] = cx;
+        nd[k] = normcx;
     }
     if (omat != 2) {  /* both cone samples' draws (e0, phi per light, samplingFunctions.h:65-82), then their trig together */
         const double e00 = smp.next();
@@ -1012,7 +1082,8 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     dv3 wt_s = mk(0, 0, 0), wh_m = mk(0, 0, 0), wo_l = mk(0, 0, 0), wi_m = mk(0, 0, 0);
     bool refl = false;
     if (omat == 0) {
-        dirs[2] = nrm(cosine_hemispheric(smp, n));  /* uniform(), samplingFunctions.h:250-261 */
+        /* uniform(), samplingFunctions.h:250-261 */
+        dirs[2] = VPT_FRAME_CSE ? nrm(cosine_hemispheric(smp, Fn)) : nrm(cosine_hemispheric(smp, n));
     } else if (omat == 2) {  /* softDielectric, samplingFunctions.h:209-235 */
         wt_s = nrm(refrax_dielectric(1.0, 1.5, wo, n));
         const double F = fresnel_die(1.0, 1.5, dot(n, wt_s), dot(n, wo));
@@ -1090,11 +1161,12 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     /* ---- the reference's arithmetic */
     dv3 mc = mk(0, 0, 0);
     double fpdf = 0, gpdf = 0, cmax = 0, wg;
+    const dv3 wolocal_f = VPT_FRAME_CSE ? nrm(to_local(Fn, wo)) : mk(0, 0, 0);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const dv3 wi = dirs[k];
-        const dv3 wilocal = nrm(to_local(n, wi));
-        const dv3 wolocal = nrm(to_local(n, wo));
+        const dv3 wilocal = VPT_FRAME_CSE ? nrm(to_local(Fn, wi)) : nrm(to_local(n, wi));
+        const dv3 wolocal = VPT_FRAME_CSE ? wolocal_f : nrm(to_local(n, wo));
         const dv3 wh = nrm(add(wilocal, wolocal));
         dv3 fr;
         if (omat == 0) fr = scl(sph_c(S, obj), (1 / VPT_PI));
@@ -1102,7 +1174,7 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         else fr = fr_microfacet(ld3(S->sph[obj].eta), ld3(S->sph[obj].kappa), wilocal, wh, wolocal, alpha, mk(0, 0, 1));
         const dv3 Le = (lt[k] == ids[k]) ? sph_rad(S, ids[k]) : mk(0, 0, 0);
         dv3 f = scl(scl(mul(Le, fr), dot(n, wi)), (1 / solid_angle_prob(cm[k])));
-        f = scl(f, transmitance(x, sph_p(S, lt[k]), sigma_t));
+        f = scl(f, VPT_MIS_REUSE ? lm_exp(sigma_t * nd[k] * -1.0) : transmitance(x, sph_p(S, lt[k]), sigma_t));
         cmax = cm[k];
         fpdf = solid_angle_prob(cmax);
         if (omat == 0) {
@@ -1123,10 +1195,15 @@ VPT_DEV dv3 mis_v2_two_lights(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     const int sourceid = hits[2] ? ids[2] : 0;
     if (omat == 0) {
         const dv3 wi = dirs[2];
-        g = add(mk(0, 0, 0), scl(scl(mul(Lb, scl(sph_c(S, obj), (1 / VPT_PI))), dot(n, wi)), (1 / hemi_cosine_prob(dot(n, wi)))));
-        gpdf = hemi_cosine_prob(dot(n, wi));
+        const double hc = hemi_cosine_prob(dot(n, wi));
+        g = add(mk(0, 0, 0), scl(scl(mul(Lb, scl(sph_c(S, obj), (1 / VPT_PI))), dot(n, wi)),
+                                 (1 / (VPT_MIS_REUSE ? hc : hemi_cosine_prob(dot(n, wi))))));
+        gpdf = hc;
         if (g.x > 0 && g.y > 0 && g.z > 0) {
-            cmax = cos_theta_max(S, sourceid, x);
+            if (VPT_MIS_REUSE && __ballot(sourceid != lt[0] && sourceid != lt[1]) == 0)
+                cmax = sourceid == lt[0] ? cm[0] : cm[1];
+            else
+                cmax = cos_theta_max(S, sourceid, x);
             fpdf = solid_angle_prob(cmax);
             wg = power_heuristic(gpdf, fpdf);
         } else {
@@ -1232,6 +1309,53 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
     return scl(mul(Le, fr), dot(n, nrm(sub(light, x))));
 }
 
+/* p_light for surface_event (VPT_PL_REUSE): the distance to the light, its square and the unit direction
+ * formed once -- visibility(), Le's 1 / |light - x|^2, wi, the final cosine and the caller's
+ * transmitance(x, light) all form them from the same light - x -- and the frame of n given (Fn).  Trs:
+ * transmitance(x, light, sigma_t). */
+#ifndef VPT_PL_REUSE
+#define VPT_PL_REUSE 1
+#endif
+template <bool COUNT, int MK = -1, int PT = -1>
+VPT_DEV dv3 p_light_nee(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray, int src,
+                        double alpha, const Frame& Fn, double sigma_t, double& Trs)
+{
+    const dv3 I = sph_rad(S, src);
+    const dv3 light = sph_p(S, src);
+    const double lr = PT == 1 ? 0.0 : S->sph[src].r;
+    const bool l3 = sph_flag(S->m_mat3, src);
+    const dv3 lx = sub(light, x);
+    const double dd = dot(lx, lx);
+    const double distance = vm_sqrt(dd);
+    const dv3 wl = nrm(lx);
+    Trs = lm_exp(sigma_t * distance * -1.0);
+    dv3 Le;
+    if (visibility_pre(S, smp, light, distance, wl, false, lr, l3)) {
+        Le = scl(I, (1 / dd));
+    } else if (VPT_LIKELY(S->n_mat3 == 0)) {
+        smp.tests(S->n);
+        Le = mk(0, 0, 0);
+    } else if (visibility_pre(S, smp, light, distance, wl, true, lr, l3)) {
+        Le = scl(I, (1 / dd));
+        Le = scl(Le, multiple_t(S, smp, x, light, 0.05 + 0.009));
+    } else {
+        Le = mk(0, 0, 0);
+    }
+    dv3 wo = scl(wray, -1);
+    wo = to_local(Fn, wo);
+    dv3 wi = to_local(Fn, wl);
+    wi = nrm(wi);
+    wo = nrm(wo);
+    dv3 fr;
+    if (mat_of<MK>(S, obj) == 1) {
+        const dv3 wh = nrm(add(wi, wo));
+        fr = fr_microfacet(ld3(S->sph[obj].eta), ld3(S->sph[obj].kappa), wi, wh, wo, alpha, mk(0, 0, 1));
+    } else {
+        fr = scl(sph_c(S, obj), (1 / VPT_PI));
+    }
+    return scl(mul(Le, fr), dot(n, wl));
+}
+
 /* freeSingleScattering (with_sigma = false), include/volumetricBasicFunctions.h:284-340, and
  * singleScattering (with_sigma = true), :225-281.  din: propagation direction (HG only).
  * For a point light the reference first casts the shadow ray (:295-304 / :236-245), then the cone
@@ -1241,18 +1365,22 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
  * point-light medium events (counting mode still adds its tests). */
 /* the shadow ray toward a point light and its radiance, volumetricBasicFunctions.h:295-304 / :236-245
  * (single_scattering's point-light branch) */
+/* mag: |lp - xt|, formed by the caller (VPT_PL_REUSE: visibility's distance and the transmittance's are
+ * the same root of the same dot product) */
 template <bool COUNT>
 VPT_DEV dv3 point_shadow_ld(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
-                            double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource)
+                            double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource, double mag)
 {
     const dv3 lp = sph_p(S, src);
     const dv3 rad = sph_rad(S, src);
     dv3 Ld = mk(0, 0, 0);
-    if (visibility(S, smp, lp, xt, false, -1.0, false)) {
+    const dv3 wl = VPT_PL_REUSE ? nrm(sub(lp, xt)) : mk(0, 0, 0);
+    if (VPT_PL_REUSE ? visibility_pre(S, smp, lp, mag, wl, false, -1.0, false)
+                     : visibility(S, smp, lp, xt, false, -1.0, false)) {
         double distanceLight = dot(sub(lp, xt), sub(lp, xt));
         dv3 Le = scl(rad, (1 / distanceLight));
-        double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, nrm(sub(lp, xt)));
-        dv3 Ls = scl(scl(Le, transmitance(xt, lp, sigma_t)), ph);
+        double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, VPT_PL_REUSE ? wl : nrm(sub(lp, xt)));
+        dv3 Ls = scl(scl(Le, VPT_PL_REUSE ? lm_exp(sigma_t * mag * -1.0) : transmitance(xt, lp, sigma_t)), ph);
         if (with_sigma) Ld = scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
         else Ld = scl(Ls, (1 / probSource));
     }
@@ -1331,7 +1459,7 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         }
     } else if (point) {
         SECT_BEGIN(swi);
-        Ld = point_shadow_ld(S, smp, xt, din, src, sigma_t, with_sigma, sigma_s, trxt, probSource);
+        Ld = point_shadow_ld(S, smp, xt, din, src, sigma_t, with_sigma, sigma_s, trxt, probSource, mag);
         SECT_END(swi, SECT_M_SHADOW_IN);
     }
     SECT_END(sw, SECT_M_SS_SHADOW);
@@ -1593,9 +1721,20 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
         vpt_sink(scl(scl(p_light<COUNT, MK, PT>(S, s2, id2, xs2, nx2, d2, src2, a2), Trs2), (1 / probSource)));
     }
 #endif
+    /* the normal's frame, formed once and shared by pLight, MISv2 and the diffuse bdsf below (VPT_FRAME_CSE;
+     * A/B ab_r06i: formed here and held through pLight's shadow ray 37.89 / 169.5 ms, formed after pLight
+     * with pLight forming its own 37.95 / 170.2, base 38.58 / 172.4) */
+    Frame Fn = {};
+    if (MK == 0 && VPT_FRAME_CSE) Fn = make_frame(nx);
     if (!plight_zero) {
-        double Trs = transmitance(xs, sph_p(S, src), sigma_t);
-        Ldp = scl(scl(p_light<COUNT, MK, PT>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+        if (MK == 0 && VPT_PL_REUSE && VPT_FRAME_CSE) {
+            double Trs;
+            const dv3 pl = p_light_nee<COUNT, MK, PT>(S, smp, id, xs, nx, p.d, src, alpha, Fn, sigma_t, Trs);
+            Ldp = scl(scl(pl, Trs), (1 / probSource));
+        } else {
+            double Trs = transmitance(xs, sph_p(S, src), sigma_t);
+            Ldp = scl(scl(p_light<COUNT, MK, PT>(S, smp, id, xs, nx, p.d, src, alpha), Trs), (1 / probSource));
+        }
     }
     SECT_END(pl, SECT_S_PLIGHT);
     SECT_BEGIN(mis);
@@ -1611,11 +1750,12 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
         vpt_opaque(id2);
         Sampler<COUNT> s2 = smp;
         vpt_opaque(s2.X);
-        vpt_sink(mis_v2_two_lights<COUNT, MK>(S, s2, id2, xs2, nx2, d2, alpha, sigma_t));
+        Frame F2 = make_frame(nx2);
+        vpt_sink(mis_v2_two_lights<COUNT, MK>(S, s2, id2, xs2, nx2, d2, alpha, sigma_t, F2));
         vpt_sink(s2.X);
     }
 #endif
-    const dv3 Ld = MK == 0 && S->n_mis == 2 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t)
+    const dv3 Ld = MK == 0 && S->n_mis == 2 ? mis_v2_two_lights<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t, Fn)
                                             : mis_v2<COUNT, MK>(S, smp, id, xs, nx, p.d, alpha, sigma_t);
     SECT_END(mis, SECT_S_MIS);
     SECT_BEGIN(bd);
@@ -1643,7 +1783,14 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
     if (cont) {
         dv3 wi = mk(0, 0, 0);
         double pdf = 0;
-        dv3 fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
+        dv3 fs;
+        if (MK == 0 && VPT_FRAME_CSE) {  /* bdsf's diffuse branch (vptShadeMethods.h:16-59) on the shared frame */
+            wi = cosine_hemispheric(smp, Fn);
+            fs = scl(sph_c(S, id), (1 / VPT_PI));
+            pdf = hemi_cosine_prob(dot(nx, wi));
+        } else {
+            fs = bdsf<COUNT, MK>(S, smp, wi, p.d, nx, pdf, id);
+        }
         wi = nrm(wi);
         double cosine = dot(nx, wi);
         p.beta = scl(scl(scl(mul(p.beta, fs), (1 / continueprob)), cosine), (1 / pdf));
