@@ -501,6 +501,12 @@ VPT_DEV Frame make_frame(dv3 n)
     coord_system(n, F.s, F.t);
     return F;
 }
+VPT_DEV void vpt_opaque(Frame& F)
+{
+    vpt_opaque(F.s);
+    vpt_opaque(F.t);
+    vpt_opaque(F.n);
+}
 VPT_DEV dv3 to_local(const Frame& F, dv3 w) { return mk(dot(F.s, w), dot(F.t, w), dot(F.n, w)); }
 VPT_DEV dv3 from_local(const Frame& F, double x1, double y1, double z1)
 {
@@ -1705,27 +1711,35 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
         plight_zero = __ballot(!zero) == 0;
         if (plight_zero) smp.tests(2 * S->n);  /* what visibility + the visibilityVPT miss would count */
     }
+    /* the normal's frame, formed once and shared by pLight, MISv2 and the diffuse bdsf below (VPT_FRAME_CSE;
+     * A/B ab_r06i: formed here and held through pLight's shadow ray 37.89 / 169.5 ms, formed after pLight
+     * with pLight forming its own 37.95 / 170.2, base 38.58 / 172.4) */
+    Frame Fn = {};
+    if (MK == 0 && VPT_FRAME_CSE) Fn = make_frame(nx);
 #if VPT_DUP == DUP_PLIGHT
     if (!plight_zero) {
         dv3 xs2 = xs, nx2 = nx, d2 = p.d;
         int id2 = id, src2 = src;
         double a2 = alpha;
+        Frame F2 = Fn;
         vpt_opaque(xs2);
         vpt_opaque(nx2);
         vpt_opaque(d2);
         vpt_opaque(id2);
         vpt_opaque(src2);
         vpt_opaque(a2);
+        vpt_opaque(F2);
         Sampler<COUNT> s2 = smp;
-        double Trs2 = transmitance(xs2, sph_p(S, src2), sigma_t);
-        vpt_sink(scl(scl(p_light<COUNT, MK, PT>(S, s2, id2, xs2, nx2, d2, src2, a2), Trs2), (1 / probSource)));
+        if (MK == 0 && VPT_PL_REUSE && VPT_FRAME_CSE) {
+            double T2;
+            const dv3 pl2 = p_light_nee<COUNT, MK, PT>(S, s2, id2, xs2, nx2, d2, src2, a2, F2, sigma_t, T2);
+            vpt_sink(scl(scl(pl2, T2), (1 / probSource)));
+        } else {
+            double Trs2 = transmitance(xs2, sph_p(S, src2), sigma_t);
+            vpt_sink(scl(scl(p_light<COUNT, MK, PT>(S, s2, id2, xs2, nx2, d2, src2, a2), Trs2), (1 / probSource)));
+        }
     }
 #endif
-    /* the normal's frame, formed once and shared by pLight, MISv2 and the diffuse bdsf below (VPT_FRAME_CSE;
-     * A/B ab_r06i: formed here and held through pLight's shadow ray 37.89 / 169.5 ms, formed after pLight
-     * with pLight forming its own 37.95 / 170.2, base 38.58 / 172.4) */
-    Frame Fn = {};
-    if (MK == 0 && VPT_FRAME_CSE) Fn = make_frame(nx);
     if (!plight_zero) {
         if (MK == 0 && VPT_PL_REUSE && VPT_FRAME_CSE) {
             double Trs;
@@ -1750,7 +1764,8 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
         vpt_opaque(id2);
         Sampler<COUNT> s2 = smp;
         vpt_opaque(s2.X);
-        Frame F2 = make_frame(nx2);
+        Frame F2 = Fn;
+        vpt_opaque(F2);
         vpt_sink(mis_v2_two_lights<COUNT, MK>(S, s2, id2, xs2, nx2, d2, alpha, sigma_t, F2));
         vpt_sink(s2.X);
     }
@@ -1773,7 +1788,16 @@ VPT_DEV void surface_event(const DevScene* __restrict__ S, Sampler<COUNT>& smp, 
         double pdf2 = 0;
         Sampler<COUNT> s2 = smp;
         vpt_opaque(s2.X);
-        dv3 fs2 = bdsf<COUNT, MK>(S, s2, wi2, d2, nx2, pdf2, id2);
+        Frame F2 = Fn;
+        vpt_opaque(F2);
+        dv3 fs2;
+        if (MK == 0 && VPT_FRAME_CSE) {
+            wi2 = cosine_hemispheric(s2, F2);
+            fs2 = scl(sph_c(S, id2), (1 / VPT_PI));
+            pdf2 = hemi_cosine_prob(dot(nx2, wi2));
+        } else {
+            fs2 = bdsf<COUNT, MK>(S, s2, wi2, d2, nx2, pdf2, id2);
+        }
         wi2 = nrm(wi2);
         vpt_sink(scl(scl(scl(mul(b2, fs2), (1 / continueprob)), dot(nx2, wi2)), (1 / pdf2)));
         vpt_sink(wi2);
