@@ -49,6 +49,10 @@ namespace vpt {
 #define VPT_LIKELY(c) __builtin_expect(!!(c), 1)
 
 #define ISECT_SQRT(x) vm_sqrt(x)
+/* the sphere tests' root with a class test for its rare arguments (vm_sqrt_isect, vpt_math.h) */
+#ifndef VPT_ISECT_CLASS
+#define VPT_ISECT_CLASS 1
+#endif
 
 /* Debug section timers (builds with -DVPT_SECTIONS=1 only; scripts/sect_stats.py): the wave's
  * s_memtime cycles spent in each section, accumulated per
@@ -255,7 +259,7 @@ VPT_DEV void sphere_test(double b, double det, int i, double& tmin, int& id, con
         return;
     }
     if (det >= 0) {
-        const double sq = ISECT_SQRT(det);
+        const double sq = VPT_ISECT_CLASS ? vm_sqrt_isect(det) : ISECT_SQRT(det);
         const double t2 = -b + sq;
         const double t1 = -b - sq;
         sphere_take(t1 < 0.0001 ? t2 : t1, i, tmin, id, contact);
@@ -981,6 +985,9 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
 #ifndef VPT_ISECT_N_GROUP
 #define VPT_ISECT_N_GROUP 5
 #endif
+#ifndef VPT_ISECT_VIDX
+#define VPT_ISECT_VIDX 1
+#endif
     /* VPT_ISECT_N_GROUP spheres per loop iteration: their records come in one batch of scalar loads
      * (one wait instead of one per sphere) */
     for (; i + VPT_ISECT_N_GROUP <= n; i += VPT_ISECT_N_GROUP) {
@@ -989,11 +996,17 @@ VPT_DEV void scene_intersect_n(const DevScene* __restrict__ S, Sampler<COUNT>& s
             const GeoSphere g = S->geo[i + j];
             const double ocx = o.x - g.px, ocy = o.y - g.py, ocz = o.z - g.pz;
             const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
+            /* the sphere index copied into a VGPR once for the N rays' id selects (VPT_ISECT_VIDX): a select
+             * cannot take it from an SGPR beside its SGPR lane mask, so each test copied it again */
+            int vi = i + j;
+#if VPT_ISECT_VIDX && defined(__HIP_DEVICE_COMPILE__)
+            if (N > 1) __asm__("v_mov_b32 %0, %1" : "=v"(vi) : "s"(i + j));
+#endif
 #pragma unroll
             for (int k = 0; k < N; ++k) {
                 const double b = ocx * d[k].x + ocy * d[k].y + ocz * d[k].z;
                 const double det = b * b - cc + g.r2;
-                sphere_test(b, det, i + j, tmin[k], id[k], contact[k]);
+                sphere_test(b, det, vi, tmin[k], id[k], contact[k]);
             }
         }
     }

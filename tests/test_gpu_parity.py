@@ -73,6 +73,29 @@ def test_device_dir_trig_cone_path_vs_glibc(gpu_tracer):
     assert bitwise_equal(gpu_tracer.math_probe(15, c, phi), c).all()  # cos(acos c) == c there
 
 
+def test_device_isect_sqrt_tiny(gpu_tracer):
+    """VPT_ISECT_CLASS (csrc/vpt_math.h vm_sqrt_isect): the sphere tests' root equals sqrt() bit for bit for
+    det = 0, inf, NaN, negative and every det >= 2^-767, and for det in (0, 2^-767) -- subnormals included,
+    where it runs the core sequence -- is a finite number below 2^-383, the bound the sphere test's
+    exactness argument needs (sq below half an ulp of any |b| >= 2^-330)"""
+    rng = np.random.default_rng(2703)
+    n = 1 << 20
+    big = np.ldexp(rng.uniform(1, 2, n), rng.integers(-767, 1024, n))
+    edge = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, -1.0, 2.0**-767, np.nextafter(2.0**-767, 0),
+                     1.7976931348623157e308])
+    x = np.concatenate([big, edge, np.tile(edge, 64)])
+    with np.errstate(invalid="ignore"):
+        ref = np.sqrt(x)
+    sel = ~((x > 0) & (x < 2.0**-767))
+    assert bitwise_equal(gpu_tracer.math_probe(21, x)[sel], ref[sel]).all()
+    # every binade below 2^-767 (normal and subnormal), whole waves of them
+    e = rng.integers(-1074, -767, n)
+    tiny = np.ldexp(rng.uniform(1, 2, n), e)
+    tiny = np.concatenate([tiny, np.array([5e-324, 1e-320, 2.0**-1022, np.nextafter(2.0**-1022, 0)])])
+    r = gpu_tracer.math_probe(21, tiny)
+    assert np.isfinite(r).all() and (r >= 0).all() and (r < 2.0**-383).all()
+
+
 def test_device_shared_reciprocal_division(gpu_tracer):
     """VPT_DIV_SHARE (csrc/vpt_math.h vm_rcp, csrc/vpt_device.h): the last three operations of the
     compiler's division on a reciprocal formed once per divisor give the division's bits for operands in
