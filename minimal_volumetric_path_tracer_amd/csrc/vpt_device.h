@@ -252,6 +252,11 @@ VPT_DEV void sphere_take(double tact, int i, double& tmin, int& id, contact_t& c
 #ifndef VPT_TAKE_IN
 #define VPT_TAKE_IN 1
 #endif
+/* ZR: the ray leaves a light's centre (vm_sqrt_isect_z) */
+#ifndef VPT_ISECT_ZERO
+#define VPT_ISECT_ZERO 1
+#endif
+template <bool ZR = false>
 VPT_DEV void sphere_test(double b, double det, int i, double& tmin, int& id, contact_t& contact)
 {
     if (!VPT_TAKE_IN) {
@@ -259,7 +264,7 @@ VPT_DEV void sphere_test(double b, double det, int i, double& tmin, int& id, con
         return;
     }
     if (det >= 0) {
-        const double sq = VPT_ISECT_CLASS ? vm_sqrt_isect(det) : ISECT_SQRT(det);
+        const double sq = (VPT_ISECT_ZERO && ZR) ? vm_sqrt_isect_z(det) : VPT_ISECT_CLASS ? vm_sqrt_isect(det) : ISECT_SQRT(det);
         const double t2 = -b + sq;
         const double t1 = -b - sq;
         sphere_take(t1 < 0.0001 ? t2 : t1, i, tmin, id, contact);
@@ -270,7 +275,7 @@ VPT_DEV void sphere_test(double b, double det, int i, double& tmin, int& id, con
 /* Sphere::intersect (include/Sphere.h:27-37) folded into intersect()
  * (include/pathTracingUtilities.h:12-36).  The sphere index is wave-uniform, so the scene
  * record comes through scalar loads. */
-template <bool COUNT>
+template <bool COUNT, bool ZR = false>
 VPT_DEV int scene_intersect(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, double& t,
                             int& id, bool skip3)
 {
@@ -287,7 +292,7 @@ VPT_DEV int scene_intersect(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
         double b = ocx * d.x + ocy * d.y + ocz * d.z;
         double cc = ocx * ocx + ocy * ocy + ocz * ocz;
         double det = b * b - cc + g.r2;
-        sphere_test(b, det, i, tmin, id, contact);
+        sphere_test<ZR>(b, det, i, tmin, id, contact);
     }
     smp.tests(skip3 ? S->n_non3 : n);
     if (contact) {
@@ -301,7 +306,7 @@ VPT_DEV int scene_intersect(const DevScene* __restrict__ S, Sampler<COUNT>& smp,
 /* scene_intersect (skip3 = false) with the spheres taken G at a time: the G dependency chains
  * up to det are formed first (independent, so they overlap), then the G square-root blocks and
  * the tmin updates in index order -- the same operations per sphere, the same result. */
-template <int G, bool COUNT>
+template <int G, bool COUNT, bool ZR = false>
 VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, double& t,
                                     int& id)
 {
@@ -322,7 +327,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         }
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            sphere_test(b[k], det[k], i + k, tmin, id, contact);
+            sphere_test<ZR>(b[k], det[k], i + k, tmin, id, contact);
         }
     }
     for (; i < n; ++i) {
@@ -331,7 +336,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
         const double b = ocx * d.x + ocy * d.y + ocz * d.z;
         const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
         const double det = b * b - cc + g.r2;
-        sphere_test(b, det, i, tmin, id, contact);
+        sphere_test<ZR>(b, det, i, tmin, id, contact);
     }
     smp.tests(n);
     if (contact) {
@@ -345,7 +350,7 @@ VPT_DEV int scene_intersect_grouped(const DevScene* __restrict__ S, Sampler<COUN
 /* scene_intersect_grouped for rays that all leave one point o, with oc = o - centre and
  * |oc|^2 of every sphere taken from oc[i][0..3] (formed once by the caller with the same operations,
  * march_origin_init): per sphere only b and det are formed -- the same values, the same result */
-template <int G, bool COUNT>
+template <int G, bool COUNT, bool ZR = false>
 VPT_DEV int scene_intersect_grouped_oc(const DevScene* __restrict__ S, Sampler<COUNT>& smp, const double (*oc)[4],
                                        dv3 d, double& t, int& id)
 {
@@ -363,13 +368,13 @@ VPT_DEV int scene_intersect_grouped_oc(const DevScene* __restrict__ S, Sampler<C
             det[k] = b[k] * b[k] - cc + S->geo[i + k].r2;
         }
 #pragma unroll
-        for (int k = 0; k < G; ++k) sphere_test(b[k], det[k], i + k, tmin, id, contact);
+        for (int k = 0; k < G; ++k) sphere_test<ZR>(b[k], det[k], i + k, tmin, id, contact);
     }
     for (; i < n; ++i) {
         const double ocx = oc[i][0], ocy = oc[i][1], ocz = oc[i][2], cc = oc[i][3];
         const double b = ocx * d.x + ocy * d.y + ocz * d.z;
         const double det = b * b - cc + S->geo[i].r2;
-        sphere_test(b, det, i, tmin, id, contact);
+        sphere_test<ZR>(b, det, i, tmin, id, contact);
     }
     smp.tests(n);
     if (contact) {
@@ -399,18 +404,21 @@ __device__ static inline void march_origin_init(const DevScene* __restrict__ S, 
 #define VPT_ISECT_GROUP_ALL 5
 #endif
 static_assert(VPT_ISECT_GROUP_ALL >= 1, "spheres are taken G >= 1 at a time");
-template <bool COUNT>
+template <bool COUNT, bool ZR = false>
 VPT_DEV int scene_isect(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d, double& t, int& id,
                         bool skip3)
 {
-    if (!skip3) return scene_intersect_grouped<VPT_ISECT_GROUP_ALL>(S, smp, o, d, t, id);
-    return scene_intersect(S, smp, o, d, t, id, skip3);
+    if (!skip3) return scene_intersect_grouped<VPT_ISECT_GROUP_ALL, COUNT, ZR>(S, smp, o, d, t, id);
+    return scene_intersect<COUNT, ZR>(S, smp, o, d, t, id, skip3);
 }
 
 /* visibility (include/pathTracingUtilities.h:39-53), skip3 = visibilityVPT
  * (include/volumetricBasicFunctions.h:92-106).  light_r: radius of the light sphere when the
  * light point is a sphere centre (exact shortcut, header comment), negative otherwise. */
-template <bool COUNT>
+/* ZR: sphere tests with vm_sqrt_isect_z (a point light's own sphere, det = 0, without the rare-argument
+ * call): the one-lane-per-pixel ray-marching and punctual kernels (A/B ab_r06o: rayMarching3 99.1 -> 94.7 ms);
+ * the pool kernel's point-light shadow rays were 0.5 % slower with it */
+template <bool COUNT, bool ZR = false>
 VPT_DEV int visibility(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 light, dv3 x, bool skip3,
                        double light_r, bool light_is3, const double (*light_oc)[4] = nullptr)
 {
@@ -424,8 +432,8 @@ VPT_DEV int visibility(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 
     lx = scl(lx, -1);
     int id = 0;
     double t;
-    if (light_oc != nullptr && !skip3) scene_intersect_grouped_oc<VPT_ISECT_GROUP_ALL>(S, smp, light_oc, lx, t, id);
-    else scene_isect(S, smp, light, lx, t, id, skip3);
+    if (light_oc != nullptr && !skip3) scene_intersect_grouped_oc<VPT_ISECT_GROUP_ALL, COUNT, ZR>(S, smp, light_oc, lx, t, id);
+    else scene_isect<COUNT, ZR>(S, smp, light, lx, t, id, skip3);
     return (t > distance || t == 0);
 }
 
@@ -1293,7 +1301,7 @@ VPT_DEV dv3 bdsf(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3& aux, 
 
 /* pLight (point-light NEE at a surface), include/vptShadeMethods.h:62-91.  PT: 1 when the caller
  * knows the light is a point (r == 0; the pool kernel's rings are keyed by it), -1 unknown. */
-template <bool COUNT, int MK = -1, int PT = -1>
+template <bool COUNT, int MK = -1, int PT = -1, bool ZR = false>  /* ZR: visibility's (iterativePathTracer: true) */
 VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj, dv3 x, dv3 n, dv3 wray, int src,
                     double alpha)
 {
@@ -1302,12 +1310,12 @@ VPT_DEV dv3 p_light(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int obj
     const double lr = PT == 1 ? 0.0 : S->sph[src].r;
     const bool l3 = sph_flag(S->m_mat3, src);
     dv3 Le;
-    if (visibility(S, smp, light, x, false, lr, l3)) {
+    if (visibility<COUNT, ZR>(S, smp, light, x, false, lr, l3)) {
         Le = scl(I, (1 / (dot(sub(light, x), sub(light, x)))));
     } else if (VPT_LIKELY(S->n_mat3 == 0)) {
         smp.tests(S->n);  /* visibilityVPT == visibility (no material-3 sphere): same miss */
         Le = mk(0, 0, 0);
-    } else if (visibility(S, smp, light, x, true, lr, l3)) {
+    } else if (visibility<COUNT, ZR>(S, smp, light, x, true, lr, l3)) {
         Le = scl(I, (1 / (dot(sub(light, x), sub(light, x)))));
         Le = scl(Le, multiple_t(S, smp, x, light, 0.05 + 0.009));
     } else {
@@ -1858,7 +1866,7 @@ VPT_DEV bool surface_event_pt(const DevScene* __restrict__ S, Sampler<COUNT>& sm
     dv3 Ld = mk(0, 0, 0);
     const int n = S->n;
     for (int l = 0; l < n; ++l)  /* wave-uniform: scalar loads of the scene */
-        if (S->sph[l].r == 0) Ld = add(p_light<COUNT, MK>(S, smp, id, x, nx, p.d, l, alpha), Ld);
+        if (S->sph[l].r == 0) Ld = add(p_light<COUNT, MK, -1, true>(S, smp, id, x, nx, p.d, l, alpha), Ld);
     Ld = add(mis_v2<COUNT, MK, false>(S, smp, id, x, nx, p.d, alpha, 0.0), Ld);
     if (smp.next() < q) return true;
     double prob = 0;
@@ -2070,6 +2078,9 @@ __device__ static dv3 trace_surface_pt(const DevScene* __restrict__ S, Sampler<C
  * VPT_MARCH_MAX_STEPS (the reference has no cap) so that every wave ends; a capped ray returns NaN. */
 #ifndef VPT_MARCH_MAX_STEPS
 #define VPT_MARCH_MAX_STEPS (1 << 22)
+#ifndef VPT_MARCH_REUSE
+#define VPT_MARCH_REUSE 1
+#endif
 #endif
 template <bool COUNT>
 __device__ static dv3 trace_ray_marching(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 o, dv3 d,
@@ -2094,9 +2105,30 @@ __device__ static dv3 trace_ray_marching(const DevScene* __restrict__ S, Sampler
         const double phase = 1 / (4 * VPT_PI);  /* isotropicPhaseFunction, volumetricBasicFunctions.h:59-62 */
         const dv3 wc = sub(lp, xt);
         const double normwc = dot(wc, wc);
-        if (visibility(S, smp, lp, xt, false, lr, l3, light_oc)) {
+        /* VPT_MARCH_REUSE: visibility's distance and the light's transmittance are the same root of normwc,
+         * its direction nrm(wc) -- formed once (visibility_pre) */
+        double dist = 0.0;
+        bool vis;
+        if (VPT_MARCH_REUSE) {  /* visibility(S, smp, lp, xt, false, lr, l3, light_oc) with its distance kept */
+            dist = vm_sqrt(normwc);
+            if (lr > 0.0001 && !(dist < lr)) {
+                smp.tests(S->n);
+                vis = false;
+            } else {
+                const dv3 lx = scl(nrm(wc), -1);
+                int idv = 0;
+                double tv;
+                if (light_oc != nullptr) scene_intersect_grouped_oc<VPT_ISECT_GROUP_ALL, COUNT, true>(S, smp, light_oc, lx, tv, idv);
+                else scene_isect<COUNT, true>(S, smp, lp, lx, tv, idv, false);
+                vis = tv > dist || tv == 0;
+            }
+        } else {
+            vis = visibility<COUNT, true>(S, smp, lp, xt, false, lr, l3, light_oc);
+        }
+        if (vis) {
             const dv3 Le = scl(sph_rad(S, src), (1 / normwc));
-            const dv3 Ls = scl(Le, (phase * transmitance(xt, lp, sigma_a + sigma_s)));
+            const double Tl = VPT_MARCH_REUSE ? lm_exp((sigma_a + sigma_s) * dist * -1.0) : transmitance(xt, lp, sigma_a + sigma_s);
+            const dv3 Ls = scl(Le, (phase * Tl));
             Li = add(Li, scl(scl(scl(Ls, T), sigma_s), step));
         } else {
             Li = add(Li, mk(0, 0, 0));
@@ -2235,7 +2267,7 @@ VPT_DEV dv3 punctual_volumetric(const DevScene* __restrict__ S, Sampler<COUNT>& 
                                 double sigma_t, double sigma_s)
 {
     const dv3 light = sph_p(S, idsource);
-    if (visibility(S, smp, light, x, true, S->sph[idsource].r, S->geo[idsource].mat3)) {
+    if (visibility<COUNT, true>(S, smp, light, x, true, S->sph[idsource].r, S->geo[idsource].mat3)) {
         dv3 Le = sph_rad(S, idsource);
         const double distanceLight = dot(sub(light, x), sub(light, x));
         Le = scl(Le, (1 / distanceLight));

@@ -372,7 +372,8 @@ __global__ void math_probe_kernel(int fn, const double* x, const double* y, doub
         r = __longlong_as_double(__double_as_longlong(inv) ^ __double_as_longlong(q));
         break;
     }
-    case 21: r = vm_sqrt_isect(a); break;  /* the sphere tests' root (VPT_ISECT_CLASS) */
+    case 21: r = vm_sqrt_isect(a); break;    /* the sphere tests' root (VPT_ISECT_CLASS) */
+    case 22: r = vm_sqrt_isect_z(a); break;  /* the shadow rays' (VPT_ISECT_ZERO) */
     default: r = a / b; break;
     }
     out[i] = r;

@@ -74,7 +74,7 @@ def test_device_dir_trig_cone_path_vs_glibc(gpu_tracer):
 
 
 def test_device_isect_sqrt_tiny(gpu_tracer):
-    """VPT_ISECT_CLASS (csrc/vpt_math.h vm_sqrt_isect): the sphere tests' root equals sqrt() bit for bit for
+    """VPT_ISECT_CLASS / VPT_ISECT_ZERO (csrc/vpt_math.h vm_sqrt_isect, vm_sqrt_isect_z): the sphere tests' root equals sqrt() bit for bit for
     det = 0, inf, NaN, negative and every det >= 2^-767, and for det in (0, 2^-767) -- subnormals included,
     where it runs the core sequence -- is a finite number below 2^-383, the bound the sphere test's
     exactness argument needs (sq below half an ulp of any |b| >= 2^-330)"""
@@ -93,6 +93,13 @@ def test_device_isect_sqrt_tiny(gpu_tracer):
     tiny = np.ldexp(rng.uniform(1, 2, n), e)
     tiny = np.concatenate([tiny, np.array([5e-324, 1e-320, 2.0**-1022, np.nextafter(2.0**-1022, 0)])])
     r = gpu_tracer.math_probe(21, tiny)
+    assert np.isfinite(r).all() and (r >= 0).all() and (r < 2.0**-383).all()
+    # the shadow rays' root (VPT_ISECT_ZERO, vm_sqrt_isect_z): zeros join the tiny range (a finite root below
+    # 2^-383 instead of the rare-argument call), everything else as above
+    with np.errstate(invalid="ignore"):
+        assert bitwise_equal(gpu_tracer.math_probe(22, x)[sel & (x != 0)], ref[sel & (x != 0)]).all()
+    z = np.concatenate([tiny, np.zeros(4096), -np.zeros(4096)])
+    r = gpu_tracer.math_probe(22, z)
     assert np.isfinite(r).all() and (r >= 0).all() and (r < 2.0**-383).all()
 
 
