@@ -11,7 +11,8 @@ C=minimal_volumetric_path_tracer_amd/csrc
 flock /tmp/vpt_build_variant.lock make -s -C "$C" vpt_host.o vpt_multi.o  # (the in-tree make takes the same lock: scripts/build_main.sh)
 # the Makefile's flags (SCHED: the scheduler strategy; SCHED= builds with the compiler's default; OPT: -O level)
 SCHED=${SCHED--mllvm -amdgpu-sched-strategy=iterative-maxocc}
-FLAGS="--offload-arch=${VARCH:-gfx950} ${OPT:--O2} -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $SCHED -Wno-unused-function $*"
+LOOPFLAGS=${LOOPFLAGS--mllvm -disable-lsr}
+FLAGS="--offload-arch=${VARCH:-gfx950} ${OPT:--O2} -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $SCHED $LOOPFLAGS -Wno-unused-function $*"
 /opt/rocm/bin/hipcc $FLAGS -c "$C/vpt_kernels.hip" -o "build_variants/vpt_kernels_$name.o"
 # the variant's own build id (sources + its flags + its name), so a result measured on a variant is
 # never recorded under the production library's id

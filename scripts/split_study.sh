@@ -8,7 +8,7 @@ EST=${1:-1}
 C=minimal_volumetric_path_tracer_amd/csrc
 TMP=$(mktemp -d)
 trap 'rm -rf "$TMP"' EXIT
-FLAGS="--offload-arch=gfx950 -O2 -std=c++17 -ffp-contract=off -fno-fast-math -mllvm -amdgpu-sched-strategy=iterative-maxocc"
+FLAGS="--offload-arch=gfx950 -O2 -std=c++17 -ffp-contract=off -fno-fast-math -mllvm -amdgpu-sched-strategy=iterative-maxocc -mllvm -disable-lsr"
 echo "# split-kernel compile study, estimator $EST (hipcc $FLAGS); per stage kernel and waves/SIMD target W:"
 echo "# vgpr (budget 512/W), sgpr, spilled VGPRs / SGPRs, scratch bytes per lane, static instructions of the kernel body"
 printf "%-10s %2s %5s %5s %6s %6s %8s %7s\n" kernel W vgpr sgpr vspill sspill scratch insts
