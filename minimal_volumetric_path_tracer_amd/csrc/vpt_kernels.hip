@@ -21,6 +21,18 @@
 #include "vpt_pool.h"
 #include "vpt_internal.h"
 
+/* the EST = 1 pool kernel comes from vpt_pool_mis.hip, compiled with flags of its own (VPT_MIS_TU;
+ * -DVPT_MIS_TU=0 instantiates it here, as the syntax checks of tests/test_knobs.py do) */
+#ifndef VPT_MIS_TU
+#define VPT_MIS_TU 1
+#endif
+#if VPT_MIS_TU
+namespace vpt {
+extern template __global__ void pool_kernel<1, false>(PoolParams P0, Medium m0, const DevScene* __restrict__ S,
+                                                      unsigned long long* counters, unsigned long long* stats);
+}  // namespace vpt
+#endif
+
 using namespace vpt;
 
 namespace {

@@ -18,15 +18,28 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
 def notes(so: str) -> str:
+    """the notes of every gfx950 code object in the .so: one offload bundle per HIP translation unit
+    (vpt_kernels.hip, vpt_pool_mis.hip), concatenated in .hip_fatbin"""
     with tempfile.TemporaryDirectory() as td:
-        fat, co = os.path.join(td, "fat.bin"), os.path.join(td, "k.co")
+        fat = os.path.join(td, "fat.bin")
         subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", so, os.path.join(td, "junk")],
                        check=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}", f"--output={co}"], check=True)
-        return subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
-                              text=True).stdout
+        blob = open(fat, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), blob)] + [len(blob)]
+        out = []
+        for k in range(len(starts) - 1):
+            part, co = os.path.join(td, f"b{k}.bin"), os.path.join(td, f"k{k}.co")
+            open(part, "wb").write(blob[starts[k]:starts[k + 1]])
+            subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}", f"--output={co}"],
+                           check=True)
+            out.append(subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                                      text=True).stdout)
+        return "\n".join(out)
 
 
 def kernels(txt: str):

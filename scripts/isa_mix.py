@@ -10,7 +10,8 @@ the dynamic budget; rare branches inside a section (libm rare arguments, the met
 static count an upper bound there.
 
 usage: python scripts/isa_mix.py <code object .co> <est 0|1> [sections.txt] > profiles/r04/isa_mix_<est>.txt
-(the .co: hipcc --cuda-device-only -c -gline-tables-only ... vpt_kernels.hip, then
+(the .co: hipcc --cuda-device-only -c -gline-tables-only ... vpt_kernels.hip -- for est 1, vpt_pool_mis.hip with
+ the Makefile's MISFLAGS, the unit that holds that kernel -- then
  clang-offload-bundler --unbundle --targets=hipv4-amdgcn-amd-amdhsa--gfx950)"""
 import collections
 import re

@@ -35,6 +35,6 @@ ARMS = {
 @pytest.mark.parametrize("arm", sorted(ARMS))
 def test_knob_arm_compiles(arm):
     cmd = [HIPCC, "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=off", "-fsyntax-only", "--cuda-device-only",
-           "-Wno-unused-command-line-argument"] + ARMS[arm] + ["vpt_kernels.hip"]
+           "-Wno-unused-command-line-argument", "-DVPT_MIS_TU=0"] + ARMS[arm] + ["vpt_kernels.hip"]
     r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
