@@ -14,11 +14,12 @@ SCHED=${SCHED--mllvm -amdgpu-sched-strategy=iterative-maxocc}
 LOOPFLAGS=${LOOPFLAGS--mllvm -disable-lsr}
 FLAGS="--offload-arch=${VARCH:-gfx950} ${OPT:--O2} -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $SCHED $LOOPFLAGS -Wno-unused-function $*"
 MISFLAGS=${MISFLAGS--mllvm -disable-machine-licm}  # the EST = 1 pool kernel's unit (csrc/Makefile MISFLAGS)
-/opt/rocm/bin/hipcc $FLAGS -c "$C/vpt_kernels.hip" -o "build_variants/vpt_kernels_$name.o"
+MAINFLAGS=${MAINFLAGS-}  # extra flags for vpt_kernels.hip only (every kernel but the EST = 1 pool kernel)
+/opt/rocm/bin/hipcc $FLAGS $MAINFLAGS -c "$C/vpt_kernels.hip" -o "build_variants/vpt_kernels_$name.o"
 /opt/rocm/bin/hipcc $FLAGS $MISFLAGS -c "$C/vpt_pool_mis.hip" -o "build_variants/vpt_pool_mis_$name.o"
 # the variant's own build id (sources + its flags + its name), so a result measured on a variant is
 # never recorded under the production library's id
-VID=$(python3 scripts/build_id.py "variant:$name | $FLAGS | $MISFLAGS")
+VID=$(python3 scripts/build_id.py "variant:$name | $FLAGS | $MAINFLAGS | $MISFLAGS")
 echo "const char* vpt_build_id(void) { return \"$VID\"; }" > "build_variants/vpt_build_id_$name.c"
 cc -O2 -fPIC -c "build_variants/vpt_build_id_$name.c" -o "build_variants/vpt_build_id_$name.o"
 /opt/rocm/bin/hipcc --offload-arch=${VARCH:-gfx950} -shared -fPIC "build_variants/vpt_kernels_$name.o" "build_variants/vpt_pool_mis_$name.o" "$C/vpt_host.o" "$C/vpt_multi.o" "build_variants/vpt_build_id_$name.o" \
