@@ -70,7 +70,8 @@ enum {
     SECT_N = 32
 };
 #if VPT_SECTIONS
-__device__ unsigned long long g_vpt_sect[3 * SECT_N];
+/* one copy per translation unit (the EST = 1 pool kernel's unit reads its own: vpt_pool_mis.hip) */
+static __device__ unsigned long long g_vpt_sect[3 * SECT_N];
 __device__ static inline __attribute__((always_inline)) uint32_t* sect_lds()
 {
     __shared__ uint32_t a[8][3 * SECT_USED];  /* per wave: cycles, entries, active lanes */

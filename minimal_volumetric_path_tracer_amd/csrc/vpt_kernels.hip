@@ -31,6 +31,9 @@ namespace vpt {
 extern template __global__ void pool_kernel<1, false>(PoolParams P0, Medium m0, const DevScene* __restrict__ S,
                                                       unsigned long long* counters, unsigned long long* stats);
 }  // namespace vpt
+#if VPT_SECTIONS
+extern "C" int vpt_mis_sections_add(unsigned long long* out);
+#endif
 #endif
 
 using namespace vpt;
@@ -1175,6 +1178,9 @@ extern "C" int vpt_debug_sections(unsigned long long* out)
     HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(vpt::g_vpt_sect), 3 * vpt::SECT_N * sizeof(unsigned long long)));
     static const unsigned long long zero[3 * vpt::SECT_N] = {};
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(vpt::g_vpt_sect), zero, sizeof(zero)));
+#if VPT_MIS_TU
+    if (vpt_mis_sections_add(out)) return vpt_fail(VPT_E_HIP, "section timers of the EST = 1 unit");
+#endif
     return VPT_OK;
 #else
     (void)out;
