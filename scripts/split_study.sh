@@ -1,14 +1,14 @@
 #!/usr/bin/env bash
 # CPU-only compile study of a split (one kernel per pool stage) design: VGPR / SGPR / spills of each stage
 # kernel of scripts/split_study.hip at 2, 3 and 4 waves per SIMD, product flags.  No GPU.
-# usage: bash scripts/split_study.sh [est] > profiles/r06/split_resources.txt
+# usage: [EXTRA=flags] bash scripts/split_study.sh [est] > profiles/r06/split_resources.txt (estimator 1: EXTRA="-mllvm -disable-machine-licm", its unit's flags)
 set -eu
 cd "$(dirname "$0")/.."
 EST=${1:-1}
 C=minimal_volumetric_path_tracer_amd/csrc
 TMP=$(mktemp -d)
 trap 'rm -rf "$TMP"' EXIT
-FLAGS="--offload-arch=gfx950 -O2 -std=c++17 -ffp-contract=off -fno-fast-math -mllvm -amdgpu-sched-strategy=iterative-maxocc -mllvm -disable-lsr"
+FLAGS="--offload-arch=gfx950 -O2 -std=c++17 -ffp-contract=off -fno-fast-math -mllvm -amdgpu-sched-strategy=iterative-maxocc -mllvm -disable-lsr ${EXTRA:-}"
 echo "# split-kernel compile study, estimator $EST (hipcc $FLAGS); per stage kernel and waves/SIMD target W:"
 echo "# vgpr (budget 512/W), sgpr, spilled VGPRs / SGPRs, scratch bytes per lane, static instructions of the kernel body"
 printf "%-10s %2s %5s %5s %6s %6s %8s %7s\n" kernel W vgpr sgpr vspill sspill scratch insts
