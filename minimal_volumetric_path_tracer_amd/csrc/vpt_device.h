@@ -1395,25 +1395,45 @@ VPT_DEV dv3 p_light_nee(const DevScene* __restrict__ S, Sampler<COUNT>& smp, int
  * (single_scattering's point-light branch) */
 /* mag: |lp - xt|, formed by the caller (VPT_PL_REUSE: visibility's distance and the transmittance's are
  * the same root of the same dot product) */
+/* the radiance of a visible point light (wl = nrm(lp - xt) under VPT_PL_REUSE) */
+template <bool COUNT>
+VPT_DEV dv3 point_shadow_value(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
+                               double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource,
+                               double mag, dv3 wl)
+{
+    const dv3 lp = sph_p(S, src);
+    const dv3 rad = sph_rad(S, src);
+    double distanceLight = dot(sub(lp, xt), sub(lp, xt));
+    dv3 Le = scl(rad, (1 / distanceLight));
+    double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, VPT_PL_REUSE ? wl : nrm(sub(lp, xt)));
+    dv3 Ls = scl(scl(Le, VPT_PL_REUSE ? lm_exp(sigma_t * mag * -1.0) : transmitance(xt, lp, sigma_t)), ph);
+    if (with_sigma) return scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
+    return scl(Ls, (1 / probSource));
+}
 template <bool COUNT>
 VPT_DEV dv3 point_shadow_ld(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
                             double sigma_t, bool with_sigma, double sigma_s, double trxt, double probSource, double mag)
 {
     const dv3 lp = sph_p(S, src);
-    const dv3 rad = sph_rad(S, src);
     dv3 Ld = mk(0, 0, 0);
     const dv3 wl = VPT_PL_REUSE ? nrm(sub(lp, xt)) : mk(0, 0, 0);
     if (VPT_PL_REUSE ? visibility_pre(S, smp, lp, mag, wl, false, -1.0, false)
-                     : visibility(S, smp, lp, xt, false, -1.0, false)) {
-        double distanceLight = dot(sub(lp, xt), sub(lp, xt));
-        dv3 Le = scl(rad, (1 / distanceLight));
-        double ph = smp.g == 0.0 ? 1 / (4 * VPT_PI) : phase_value(smp.g, din, VPT_PL_REUSE ? wl : nrm(sub(lp, xt)));
-        dv3 Ls = scl(scl(Le, VPT_PL_REUSE ? lm_exp(sigma_t * mag * -1.0) : transmitance(xt, lp, sigma_t)), ph);
-        if (with_sigma) Ld = scl(scl(scl(Ls, trxt), sigma_s), (1 / probSource));
-        else Ld = scl(Ls, (1 / probSource));
-    }
+                     : visibility(S, smp, lp, xt, false, -1.0, false))
+        Ld = point_shadow_value(S, smp, xt, din, src, sigma_t, with_sigma, sigma_s, trxt, probSource, mag, wl);
     return Ld;
 }
+
+/* Single scattering toward a point light (VPT_SS_FUSE): the light cone's ray can only score through
+ * src == idHit, and its nearest contact is the light's r = 0 sphere only if that sphere's own test has
+ * det >= 0.  A lane whose light sphere gives det < 0 (NaN included) on the cone ray -- formed here with
+ * scene_isect's operations -- therefore ends in the shadow-ray branch whatever the other spheres give
+ * (unless src == 0 and nothing is hit: idHit keeps its initial 0, so src == 0 lanes are left out), and
+ * it casts its shadow ray in the cone ray's pass instead (its origin and direction per lane), with
+ * visibility_pre's test on the result.  The shadow rays left for the divergent second pass are those of
+ * lanes whose cone ray met another sphere first. */
+#ifndef VPT_SS_FUSE
+#define VPT_SS_FUSE 1
+#endif
 
 template <bool COUNT, int LT = -1>  /* LT: 1 point light, 0 not, -1 unknown (read r) */
 VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& smp, dv3 xt, dv3 din, int src,
@@ -1470,10 +1490,26 @@ VPT_DEV dv3 single_scattering(const DevScene* __restrict__ S, Sampler<COUNT>& sm
         vpt_sink(id2);
     }
 #endif
-    scene_isect(S, smp, xt, wl, tdist, idHit, false);
+    bool shl = false;  /* VPT_SS_FUSE: this lane's pass casts its shadow ray */
+    dv3 wls = mk(0, 0, 0);
+    if (VPT_SS_FUSE && VPT_PL_REUSE && point) {
+        /* (geo[src] holds lp and r2 = r r = +0 for a point light: the same operands) */
+        const double ocx = xt.x - lp.x, ocy = xt.y - lp.y, ocz = xt.z - lp.z;
+        const double b = ocx * wl.x + ocy * wl.y + ocz * wl.z;
+        const double cc = ocx * ocx + ocy * ocy + ocz * ocz;
+        const double det = b * b - cc + 0.0;
+        shl = src != 0 && !(det >= 0);
+        if (shl) wls = nrm(sub(lp, xt));
+    }
+    if (VPT_SS_FUSE && VPT_PL_REUSE && point) scene_isect(S, smp, shl ? lp : xt, shl ? scl(wls, -1) : wl, tdist, idHit, false);
+    else scene_isect(S, smp, xt, wl, tdist, idHit, false);
     SECT_END(si, SECT_M_SS_ISECT);
     SECT_BEGIN(sw);
-    if (src == idHit) {
+    if (shl) {
+        smp.tests(S->n);  /* the shadow ray (cast in the pass above) or the cone ray: each is counted */
+        if (tdist > mag || tdist == 0)  /* visibility_pre */
+            Ld = point_shadow_value(S, smp, xt, din, src, sigma_t, with_sigma, sigma_s, trxt, probSource, mag, wls);
+    } else if (src == idHit) {
         if (point) smp.tests(S->n);  /* the shadow ray the reference casts first (result overwritten) */
         /* a point light's cone (cmax == 1: prob_wl = +inf) scores Ls * (1 / inf) = +-0 with Ls finite
          * (SURVEY H5); zero_ok: the caller's update absorbs a signed zero (finite throughput and

@@ -26,7 +26,8 @@ ARMS = {
     # det >= 0 branch, branchy frames, exec-masked rare paths, plain divisions, general cone acos/cos
     "round6_off": ["-DVPT_TAKE_SEL=0", "-DVPT_TAKE_IN=0", "-DVPT_FRAME_SEL=0", "-DVPT_RARE_BALLOT=0",
                    "-DVPT_DIV_SHARE=0", "-DVPT_ACOS_CONE=0", "-DVPT_COS_ACOS_C=0", "-DVPT_FRAME_CSE=0",
-                   "-DVPT_MIS_REUSE=0", "-DVPT_PL_REUSE=0", "-DVPT_ISECT_CLASS=0", "-DVPT_ISECT_VIDX=0", "-DVPT_ISECT_ZERO=0", "-DVPT_MARCH_REUSE=0"],
+                   "-DVPT_MIS_REUSE=0", "-DVPT_PL_REUSE=0", "-DVPT_ISECT_CLASS=0", "-DVPT_ISECT_VIDX=0", "-DVPT_ISECT_ZERO=0", "-DVPT_MARCH_REUSE=0",
+                   "-DVPT_SS_FUSE=0"],
     "dup_sections": ["-DVPT_DUP=3"],  # a VPT_DUP measurement build (scripts/dup_pmc.sh)
 }
 
